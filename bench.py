@@ -1,0 +1,194 @@
+"""Benchmark: top-k retrieval QPS + achieved HBM GB/s (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], the config the metric is quoted on):
+  10M × 768 bf16 corpus (synthetic, counter-based generator, rows L2-normalised), batches of 256
+  queries (bf16), brute-force top-10.  With --gpus N the corpus is row-sharded over N ranks
+  (one process per GPU, torch.distributed backend "nccl" = RCCL) and each step ends with the
+  all-gather of per-shard top-k + merge (rfx.dist) — total work fixed => "scaling": "strong".
+A step = one batch: fused MFMA scan + per-shard merge (+ all-gather + global merge for N > 1),
+inputs already resident in HBM.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--nq Q] [--k K] [--dim D]
+                       [--dtype bf16|f16|f32] [--no-cpu-baseline]
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "rag-foundation_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "top-k retrieval QPS + achieved HBM GB/s, 10M×768 k=10, 1/2/4/8 MI355X"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec; 6.29 TB/s measured float4 copy)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--dim", type=int, default=768)
+    ap.add_argument("--nq", type=int, default=256)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-sample-rows", type=int, default=1_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor()
+
+
+def load_pmc_traffic(workload_key):
+    """HBM bytes per scan launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(p))
+        e = d.get(workload_key)
+        return None if e is None else float(e["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from rfx import dist as rdist
+    from rfx.index import DeviceIndex, synth_rows, topk_merge
+
+    dev = torch.device("cuda", local)
+    r0, r1 = rdist.shard_range(a.rows, rank, world)
+    n_local = r1 - r0
+    ix = DeviceIndex(a.dim, a.dtype, local, capacity=n_local)
+    ix.add_synthetic(a.seed, n_local, gen_row0=r0)
+    q = synth_rows(a.seed + 1, 0, a.nq, a.dim, a.dtype, local)
+    kern, n_cand = ix.plan(a.nq, a.k)
+    ws = torch.empty(max(ix.workspace_bytes(a.nq, a.k), 1), dtype=torch.uint8, device=dev)
+    cs = torch.empty((a.nq, n_cand), dtype=torch.float32, device=dev)
+    cr = torch.empty((a.nq, n_cand), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize()
+
+    from rfx._lib import check, lib, ptr, stream_ptr
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        check(lib.rfx_scan_topk(ix.handle, ptr(q), a.nq, a.k, ptr(cs), ptr(cr), ptr(ws), ws.numel(),
+                                stream_ptr(stream)))
+        if ev is not None:
+            ev[1].record(stream)
+        s, r = topk_merge(cs, cr, a.k, row_offset=r0, stream=stream)
+        if world > 1:
+            s, r = rdist.gather_merge(s, r, a.k, topk_merge)
+        return s, r
+
+    for _ in range(a.warmup):
+        step()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        out = step(evs[i])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    scan_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
+    if world > 1:
+        t = torch.tensor([elapsed, scan_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, scan_ms = float(t[0]), float(t[1])
+
+    esz = {"bf16": 2, "f16": 2, "f32": 4}[a.dtype]
+    # algorithmic bytes of one scan launch on the largest shard: rows read once,
+    # queries read once, (score,row) results written once.
+    n_max = rdist.shard_range(a.rows, 0, world)[1]
+    alg_bytes = n_max * a.dim * esz + a.nq * a.dim * esz + a.nq * a.k * 12
+    achieved = alg_bytes / (scan_ms * 1e-3) / 1e9
+    qps = a.nq * a.steps / elapsed
+    workload_key = f"{a.rows}x{a.dim}-{a.dtype}-nq{a.nq}-k{a.k}-g{world}"
+    result = {
+        "metric": METRIC,
+        "value": round(qps, 1),
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": a.dtype,
+        "data": "synthetic (splitmix64 counter-based corpus + queries, rows L2-normalised; oracle/synth.py)",
+        "config": {"workload": f"cfg3: {a.rows}x{a.dim} {a.dtype} corpus row-sharded over {world} GPU(s), "
+                               f"{a.nq} queries/batch, brute-force top-{a.k}",
+                   "rows": a.rows, "dim": a.dim, "nq": a.nq, "k": a.k, "parallelism": f"rowshard{world}",
+                   "scan_kernel": "mfma" if kern == 1 else "valu"},
+        "achieved_hbm_gbps_per_gpu": round(achieved, 1),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": load_pmc_traffic(workload_key),
+                     "kernel": "scan_mfma_kernel" if kern == 1 else "scan_valu_kernel",
+                     "kernel_ms": round(scan_ms, 4), "alg_bytes_per_launch": alg_bytes},
+    }
+
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(ix, q, a)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(ix, q, a):
+    """Oracle (numpy) top-k on the host cores over a bounded row sample, extrapolated to the
+    full corpus (QPS = nq / (t_sample * rows / sample_rows))."""
+    import numpy as np
+
+    from oracle import baseline, synth
+
+    n = min(a.cpu_sample_rows, ix.rows)
+    stored = ix.read(0, n).cpu()
+    if a.dtype == "bf16":
+        stored = stored.view(torch.int16).numpy().view(np.uint16)
+    else:
+        stored = stored.numpy()
+    qh = q.cpu()
+    q64 = synth.to_f64(qh.view(torch.int16).numpy().view(np.uint16) if a.dtype == "bf16" else qh.numpy(), a.dtype)
+    secs, _, _ = baseline.time_topk(stored, a.dtype, q64, a.k)
+    full = secs * a.rows / n
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    return {"value": round(a.nq / full, 2), "unit": "queries/s", "cores": threads, "kind": "port",
+            "sample": f"oracle numpy top-{a.k} of {a.nq} queries over rows 0..{n} of the same corpus "
+                      f"({secs:.2f} s), extrapolated x{a.rows / n:.1f} to {a.rows} rows",
+            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
+            "mock_retriever_us_per_call": round(baseline.time_mock_plumbing(), 2)}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,153 @@
+/*
+ * rfx.h — C ABI of the MI355X-native embedding-index + top-k retrieval path.
+ *
+ * This library replaces the arithmetic that the reference (Sapphire-Bridge/rag-foundation)
+ * delegates to Gemini File Search behind its Retriever/LLM adapter:
+ *   - index write  : GeminiRag.upload_file          backend/app/services/gemini_rag.py:307-352
+ *                    (mock: MockGeminiRag.upload_file gemini_rag.py:614-629), called from the
+ *                    ingestion worker's index step   backend/app/services/ingestion.py:45-52,225
+ *   - retrieval    : GeminiRag.ask_stream / ask     gemini_rag.py:481-551 (FileSearch tool
+ *                    gemini_rag.py:463-469); mock    gemini_rag.py:656-694,704-718
+ *   - removal      : delete_document_from_store     gemini_rag.py:392-424 (mock 699-702)
+ *                    delete_store                    gemini_rag.py:354-390 (mock 696-697)
+ * The reference has no FFI of its own (it is pure Python); these entry points are what its
+ * adapter would bind through ctypes (see INTEGRATION.md for the binding stub).
+ *
+ * Conventions
+ *   - Every function returns int: RFX_OK (0) or an RFX_E* code; rfx_last_error() gives a
+ *     thread-local message for the last failure on the calling thread.
+ *   - Pointers named *_d are DEVICE pointers (caller-owned, e.g. torch tensors' data_ptr()),
+ *     *_h are HOST pointers.  `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *   - Only the index storage is owned by the library (behind an rfx_index_t handle).
+ *   - Rows are identified by int64 row ids (dense, in insertion order).  Result padding for
+ *     k > live rows is (score = -inf, row = -1).
+ *   - Ranking rule everywhere: score descending, then row id ascending (deterministic ties).
+ */
+#ifndef RFX_H
+#define RFX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes ---------------------------------------------------------------------- */
+#define RFX_OK 0
+#define RFX_EINVAL 1   /* bad argument / shape (maps to ValueError / RuntimeError)        */
+#define RFX_ENOMEM 2   /* device or host allocation failed                                  */
+#define RFX_EDEVICE 3  /* HIP runtime error                                                 */
+#define RFX_EIO 4      /* file read/write failed                                            */
+#define RFX_EBUSY 5    /* transient: device busy / queue timeout (maps to TimeoutError,     */
+                       /* i.e. RETRYABLE_EXCEPTIONS, gemini_rag.py:22-27)                   */
+#define RFX_EUNSUPPORTED 6 /* configuration not supported by any kernel                     */
+
+/* ---- element types of the vector store --------------------------------------------------- */
+#define RFX_F32 0
+#define RFX_BF16 1
+#define RFX_F16 2
+
+typedef uint64_t rfx_index_t;
+
+/* ---- library ------------------------------------------------------------------------------ */
+/* Thread-local message describing the last error on this thread ("" if none). */
+const char* rfx_last_error(void);
+/* ABI version (major*10000 + minor*100 + patch). */
+int rfx_version(void);
+/* Number of visible HIP devices. */
+int rfx_device_count(int* out_n);
+/* Bind the calling thread to a device (process-level singleton per device).
+ * Replaces the client construction in get_rag_client() gemini_rag.py:721-725. */
+int rfx_init(int device);
+
+/* ---- vector store (index) ----------------------------------------------------------------
+ * Replaces the File Search store namespace: create_store gemini_rag.py:271-304 / mock 610-612.
+ * dim must be a multiple of 64; capacity is rounded up internally and grows on demand. */
+int rfx_index_create(int device, int dim, int dtype, int64_t capacity, rfx_index_t* out);
+/* Drops the store (delete_store gemini_rag.py:354-390). */
+int rfx_index_destroy(rfx_index_t h);
+int rfx_index_info(rfx_index_t h, int* dim, int* dtype, int64_t* rows, int64_t* capacity,
+                   int64_t* live_rows);
+int rfx_index_reserve(rfx_index_t h, int64_t capacity);
+/* Append n already-normalised rows of the index dtype (vector-store write of upload_file,
+ * gemini_rag.py:319-327).  src_is_device selects hipMemcpy direction. */
+int rfx_index_add(rfx_index_t h, const void* vecs, int64_t n, int src_is_device,
+                  int64_t* out_first_row, void* stream);
+/* Append n synthetic rows generated on the device from the counter-based generator
+ * (splitmix64, seed, generator row id) — bench/test corpora, identical to oracle/synth.py.
+ * Generator rows are gen_row0 .. gen_row0+n-1 (gen_row0 < 0: continue at the index's row
+ * count); a row-sharded corpus passes its global row offset. */
+int rfx_index_add_synthetic(rfx_index_t h, uint64_t seed, int64_t gen_row0, int64_t n,
+                            int64_t* out_first_row, void* stream);
+/* Tombstone rows (delete_document_from_store gemini_rag.py:392-424): the rows' vectors are
+ * overwritten with NaN on the device so no scan can ever rank them. */
+int rfx_index_tombstone(rfx_index_t h, const int64_t* rows_h, int64_t n, void* stream);
+/* Copy rows [row0, row0+n) to dst (device or host). */
+int rfx_index_read(rfx_index_t h, int64_t row0, int64_t n, void* dst, int dst_is_device, void* stream);
+/* Device pointer to row 0 (row-major [capacity][dim] of dtype).  Valid until next add. */
+int rfx_index_data(rfx_index_t h, void** out_ptr);
+/* Persist / restore (ingestion deletes the source file, ingestion.py:341, so the index must
+ * survive the process).  Format documented in DESIGN.md §Persistence. */
+int rfx_index_save(rfx_index_t h, const char* path);
+int rfx_index_load(const char* path, int device, rfx_index_t* out);
+
+/* ---- search ---------------------------------------------------------------------------------
+ * Retrieval slice of ask_stream (gemini_rag.py:517-551; mock 673-694): brute-force inner
+ * product (cosine on normalised rows) of nq queries against all live rows, top-k per query.
+ * queries_d: [nq][dim] in the index dtype.  Outputs [nq][k] (device).  ws_d/ws_bytes: caller
+ * workspace of at least rfx_search_workspace_bytes(h, nq, k) bytes.  k <= 64. */
+int rfx_search_workspace_bytes(rfx_index_t h, int64_t nq, int k, size_t* out_bytes);
+int rfx_search(rfx_index_t h, const void* queries_d, int64_t nq, int k, float* out_scores_d,
+               int64_t* out_rows_d, void* ws_d, size_t ws_bytes, void* stream);
+/* The two halves of rfx_search, exposed so callers (multi-GPU merge, benchmarks) can time or
+ * interleave them: the fused scan writes n_cand candidates per query (sorted partial lists,
+ * cand_scores_d/cand_rows_d: [nq][n_cand], rows local int32), then the merge.  rfx_scan_topk
+ * uses the front of ws_d for query staging (any ws sized by rfx_search_workspace_bytes). */
+int rfx_scan_plan(rfx_index_t h, int64_t nq, int k, int* out_kernel /* 0 VALU, 1 MFMA */,
+                  int64_t* out_n_cand /* candidates per query */);
+int rfx_scan_topk(rfx_index_t h, const void* queries_d, int64_t nq, int k, float* cand_scores_d,
+                  int32_t* cand_rows_d, void* ws_d, size_t ws_bytes, void* stream);
+/* Merge per-query candidate lists into the final top-k.  rows are int32 (rows_are_i64 = 0) or
+ * int64 (1); row_offset is added to every returned row (shard base for multi-GPU). */
+int rfx_topk_merge(const float* cand_scores_d, const void* cand_rows_d, int rows_are_i64,
+                   int64_t nq, int64_t n_cand, int k, int64_t row_offset, float* out_scores_d,
+                   int64_t* out_rows_d, void* stream);
+
+/* ---- text → features (host) ---------------------------------------------------------------
+ * The reference has no chunker/tokeniser of its own (chunking_config is forwarded to Gemini,
+ * gemini_rag.py:324-326).  These restate the only tokeniser in the reference —
+ * scripts/benchmark/metrics.py:13-19 (_normalize: lower, [^a-z0-9\s] -> ' ', split, drop
+ * articles) — on UTF-8 bytes, after the caller has applied str.lower() for non-ASCII input.
+ *
+ * Whitespace chunking (Gemini white_space_config semantics): windows of max_tokens
+ * whitespace-delimited tokens, consecutive windows overlapping by `overlap` tokens.
+ * out_spans_h: [cap][2] byte offsets (start, end).  Returns the count in *out_n (if > cap
+ * only the first cap are written). */
+int rfx_chunk_whitespace(const char* text, int64_t len, int max_tokens, int overlap,
+                         int64_t* out_spans_h, int64_t cap, int64_t* out_n);
+/* Hashed bag-of-words features for n chunks (spans into text): CSR with per-chunk sorted
+ * unique buckets (V a power of two) and signed counts clamped to [-256, 256]. */
+int rfx_featurize(const char* text, const int64_t* spans_h, int64_t n, int V,
+                  uint64_t hash_seed, int32_t* indptr_h /* n+1 */, int32_t* bucket_h,
+                  int16_t* count_h, int64_t cap_nnz, int64_t* out_nnz);
+
+/* ---- embedding (device) ---------------------------------------------------------------------
+ * Chunk-embedding dense contraction on MFMA: E = F · W, F = densified CSR features [n][V]
+ * (bf16), W = seeded projection [V][dim] (stored transposed, bf16), then exact L2
+ * normalisation and cast to out_dtype.  Bit-identical to oracle/embed.py. */
+int rfx_embed_weights(int V, int dim, uint64_t seed, void* wt_d /* [dim][V] bf16 */,
+                      void* stream);
+int rfx_embed_workspace_bytes(int64_t n, int V, size_t* out_bytes);
+int rfx_embed(const int32_t* indptr_d, const int32_t* bucket_d, const int16_t* count_d,
+              int64_t n, int V, const void* wt_d, int dim, void* out_d, int out_dtype,
+              void* ws_d, size_t ws_bytes, void* stream);
+
+/* ---- synthetic rows (tests / bench) --------------------------------------------------------- */
+int rfx_synth_rows(uint64_t seed, int64_t row0, int64_t n, int dim, int dtype, void* out_d,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RFX_H */

@@ -1,0 +1,96 @@
+"""Brute-force inner-product top-k (oracle restatement of the scan + merge kernels).
+
+Ranking rule: score descending, then row id ascending.  Scores are
+accumulated in float64 over the exactly-widened stored values.  Rows whose stored vector
+contains NaN (tombstones) are never returned; results are padded with (-inf, -1).
+"""
+import numpy as np
+
+
+def topk(queries64: np.ndarray, rows64: np.ndarray, k: int, row_block: int = 1 << 18):
+    """Return (scores f64 [nq][k], rows int64 [nq][k]) for float64 inputs."""
+    queries64 = np.asarray(queries64, dtype=np.float64)
+    nq = queries64.shape[0]
+    best_s = np.full((nq, 0), -np.inf)
+    best_r = np.zeros((nq, 0), dtype=np.int64)
+    n = rows64.shape[0]
+    for b in range(0, n, row_block):
+        blk = np.asarray(rows64[b:b + row_block], dtype=np.float64)
+        dead = np.isnan(blk).any(axis=1)
+        s = queries64 @ np.where(dead[:, None], 0.0, blk).T     # [nq][B]
+        s[:, dead] = -np.inf
+        rows = np.arange(b, b + blk.shape[0], dtype=np.int64)
+        m = min(k, s.shape[1])
+        part = np.argpartition(-s, m - 1, axis=1)[:, :m]
+        kth = np.take_along_axis(s, part, axis=1).min(axis=1, keepdims=True)
+        keep = (s >= kth) & ~dead[None, :]
+        cnt = keep.sum(axis=1)
+        width = int(cnt.max()) + best_s.shape[1] if nq else 0
+        cs = np.full((nq, width), -np.inf)
+        cr = np.full((nq, width), np.iinfo(np.int64).max, dtype=np.int64)
+        for i in range(nq):
+            ks = s[i][keep[i]]
+            kr = rows[keep[i]]
+            allr = np.concatenate([best_r[i], kr])
+            alls = np.concatenate([best_s[i], ks])
+            cs[i, :len(alls)] = alls
+            cr[i, :len(allr)] = allr
+        order = np.lexsort((cr, -cs), axis=1)[:, :k]
+        best_s = np.take_along_axis(cs, order, axis=1)
+        best_r = np.take_along_axis(cr, order, axis=1)
+        best_r[best_r == np.iinfo(np.int64).max] = -1
+        best_r[best_r < 0] = -1
+        best_s[best_r < 0] = -np.inf
+        # drop padding so the next merge sees only real candidates
+        width = int((best_r >= 0).sum(axis=1).max()) if nq else 0
+        best_s, best_r = best_s[:, :width], best_r[:, :width]
+        best_r = np.where(best_r < 0, np.iinfo(np.int64).max, best_r)
+    out_s = np.full((nq, k), -np.inf)
+    out_r = np.full((nq, k), -1, dtype=np.int64)
+    w = min(k, best_s.shape[1])
+    out_s[:, :w] = best_s[:, :w]
+    out_r[:, :w] = np.where(best_r[:, :w] == np.iinfo(np.int64).max, -1, best_r[:, :w])
+    out_s[out_r < 0] = -np.inf
+    return out_s, out_r
+
+
+def check_topk(gpu_s, gpu_r, ref_s, ref_r, scores_of, tol=1e-5, tie_band=2e-6):
+    """Parity rule.  Row lists must be identical, except that two rows whose
+    reference scores differ by <= tie_band may appear in either order and may swap across the
+    k-th boundary.  GPU scores must be within `tol` of the reference fp64 score of the SAME row.
+    `scores_of(q, rows)` returns reference fp64 scores for arbitrary rows of query q.
+    Returns a list of human-readable problems (empty = pass)."""
+    problems = []
+    nq, k = ref_r.shape
+    for q in range(nq):
+        g, r = gpu_r[q], ref_r[q]
+        if np.array_equal(g, r):
+            live = g >= 0
+            if live.any():
+                d = np.abs(gpu_s[q][live].astype(np.float64) - ref_s[q][live])
+                if d.max() > tol:
+                    problems.append(f"q{q}: score err {d.max():.3g} > {tol}")
+            continue
+        if (g < 0).sum() != (r < 0).sum():
+            problems.append(f"q{q}: live count differs {g.tolist()} vs {r.tolist()}")
+            continue
+        live = g >= 0
+        sg = scores_of(q, g[live])
+        d = np.abs(gpu_s[q][live].astype(np.float64) - sg)
+        if d.max() > tol:
+            problems.append(f"q{q}: score err {d.max():.3g} > {tol}")
+        kth = ref_s[q][live.sum() - 1]
+        if (sg < kth - tie_band).any():
+            problems.append(f"q{q}: returned row below k-th score band: {g.tolist()} vs {r.tolist()}")
+        # order: GPU order must be non-increasing in reference score up to the tie band
+        if (np.diff(sg) > tie_band).any():
+            problems.append(f"q{q}: order violates ranking beyond tie band")
+        # any mismatched position must be explained by a near-tie
+        for a, b in zip(g[live], r[live]):
+            if a != b:
+                sa = scores_of(q, np.array([a]))[0]
+                sb = scores_of(q, np.array([b]))[0]
+                if abs(sa - sb) > tie_band:
+                    problems.append(f"q{q}: row {a} vs {b} differ by {abs(sa - sb):.3g} (> tie band)")
+                    break
+    return problems

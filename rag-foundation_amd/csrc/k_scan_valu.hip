@@ -1,0 +1,357 @@
+// k_scan_valu.hip — synthetic row generator, VALU fused scan + top-k, and top-k merge.
+//
+// Path: query×corpus inner-product scan + per-query top-k (the retrieval half of
+// GeminiRag.ask_stream, backend/app/services/gemini_rag.py:517-551, which the reference runs
+// remotely).  This file holds the small-batch (nq <= 8) scan; batched bf16/f16 queries go to
+// the MFMA scan in k_scan_mfma.hip.
+//
+// Data layout in HBM: the vector store is row-major [rows][dim] of the index dtype, rows
+// 16-B aligned (dim % 64 == 0).  A wave scans a contiguous row range; each 16-lane DPP row of
+// the wave owns one corpus row per step (4 rows per wave-instruction, 256 contiguous bytes
+// per row per load), so every load is a full-line coalesced dwordx4.
+#include "rfx_device.h"
+#include "rfx_kernels.h"
+
+namespace rfx {
+
+// ---------------------------------------------------------------------------------------
+// Synthetic rows: value(seed,row,col) = odd integer n in (-2^24, 2^24) from splitmix64; row
+// normalised exactly (int64 sum of squares, f64 sqrt/div) then rounded to f32 then dtype.
+// oracle/synth.py is the CPU restatement (bit-identical).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ int32_t synth_raw(uint64_t base, uint64_t idx) {
+  const uint64_t u = splitmix64(base + idx);
+  return (int32_t)(2u * (uint32_t)(u >> 40)) + 1 - (1 << 24);
+}
+
+template <int DT>
+__global__ __launch_bounds__(256) void synth_rows_kernel(uint64_t base, int64_t row0, int64_t n,
+                                                         int dim, void* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < n; i += nwaves) {
+    const uint64_t rowkey = (uint64_t)(row0 + i) * (uint64_t)dim;
+    long long ss = 0;
+    for (int c = lane; c < dim; c += 64) {
+      const long long v = synth_raw(base, rowkey + c);
+      ss += v * v;
+    }
+#pragma unroll
+    for (int off = 32; off; off >>= 1) ss += __shfl_xor(ss, off);
+    const double r = 1.0 / sqrt((double)ss);
+    for (int c = lane; c < dim; c += 64) {
+      const float x = (float)((double)synth_raw(base, rowkey + c) * r);
+      if constexpr (DT == RFX_F32) {
+        ((float*)out)[i * dim + c] = x;
+      } else if constexpr (DT == RFX_BF16) {
+        ((uint16_t*)out)[i * dim + c] = f32_to_bf16(x);
+      } else {
+        ((uint16_t*)out)[i * dim + c] = f32_to_f16(x);
+      }
+    }
+  }
+}
+
+void launch_synth_rows(uint64_t seed, int64_t row0, int64_t n, int dim, int dtype, void* out,
+                       hipStream_t st) {
+  const uint64_t base = splitmix64(seed);
+  const int64_t waves = n < 1 ? 1 : n;
+  const int blocks = (int)std::min<int64_t>((waves + 3) / 4, 8192);
+  if (dtype == RFX_F32)
+    hipLaunchKernelGGL(synth_rows_kernel<RFX_F32>, dim3(blocks), dim3(256), 0, st, base, row0, n, dim, out);
+  else if (dtype == RFX_BF16)
+    hipLaunchKernelGGL(synth_rows_kernel<RFX_BF16>, dim3(blocks), dim3(256), 0, st, base, row0, n, dim, out);
+  else
+    hipLaunchKernelGGL(synth_rows_kernel<RFX_F16>, dim3(blocks), dim3(256), 0, st, base, row0, n, dim, out);
+}
+
+// Fill rows with quiet NaN (tombstone): NaN scores never pass the ranking rule.
+__global__ void nan_rows_kernel(uint8_t* __restrict__ X, const int64_t* __restrict__ rows, int64_t n,
+                                int64_t row_bytes, uint32_t pattern) {
+  const int64_t r = blockIdx.x;
+  if (r >= n) return;
+  uint8_t* p = X + rows[r] * row_bytes;
+  for (int64_t b = threadIdx.x * 4; b < row_bytes; b += blockDim.x * 4) *(uint32_t*)(p + b) = pattern;
+}
+
+void launch_nan_rows(void* X, const int64_t* rows_d, int64_t n, int64_t row_bytes, int dtype,
+                     hipStream_t st) {
+  if (n <= 0) return;
+  const uint32_t pattern = dtype == RFX_F32 ? 0x7fc00000u : (dtype == RFX_BF16 ? 0x7fc07fc0u : 0x7e007e00u);
+  hipLaunchKernelGGL(nan_rows_kernel, dim3((unsigned)n), dim3(256), 0, st, (uint8_t*)X, rows_d, n,
+                     row_bytes, pattern);
+}
+
+// ---------------------------------------------------------------------------------------
+// VALU fused scan + top-k (nq <= 8 per launch slice).
+//   X      : [nrows][D] dtype DT
+//   Qf     : [nq][D] f32 (exact widening of the index-dtype queries)
+//   output : cand_s/cand_r [nq][n_lists][K], n_lists = gridDim.x * 4 (one list per wave)
+// Algorithmic bytes per row: D * esz (the row is read once for all NQT queries).
+// ---------------------------------------------------------------------------------------
+template <int DT>
+__device__ __forceinline__ float elem(const uint4& v, int e) {
+  const uint32_t w = (&v.x)[DT == RFX_F32 ? e : (e >> 1)];
+  if constexpr (DT == RFX_F32) {
+    return __uint_as_float(w);
+  } else if constexpr (DT == RFX_BF16) {
+    return (e & 1) ? __uint_as_float(w & 0xffff0000u) : __uint_as_float(w << 16);
+  } else {
+    return f16_to_f32((e & 1) ? (uint16_t)(w >> 16) : (uint16_t)(w & 0xffffu));
+  }
+}
+
+template <int DT, int NQT, int K, int VPL>
+__global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restrict__ X, int nrows, int D,
+                                                        const float* __restrict__ Qf, int nq,
+                                                        int rows_per_wave, float* __restrict__ cand_s,
+                                                        int* __restrict__ cand_r, int n_lists) {
+  constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
+  constexpr int EPV = 16 / ESZ;
+  extern __shared__ __attribute__((aligned(16))) float q_lds[];  // [NQT][D]
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, g = lane >> 4, j = lane & 15;
+  const int q0 = blockIdx.y * NQT;
+  const int nqt = min(NQT, nq - q0);
+  for (int i = tid; i < NQT * D; i += 256) {
+    const int qi = i / D;
+    q_lds[i] = qi < nqt ? Qf[(int64_t)(q0 + qi) * D + (i - qi * D)] : 0.f;
+  }
+  __syncthreads();
+
+  const int VPR = D * ESZ / 16;
+  const int64_t RB = (int64_t)D * ESZ;
+  const int wave_g = blockIdx.x * 4 + (tid >> 6);
+  const int wb = (int)min((int64_t)wave_g * rows_per_wave, (int64_t)nrows);
+  const int we = (int)min((int64_t)wb + rows_per_wave, (int64_t)nrows);
+
+  WaveList<K> L[NQT];
+#pragma unroll
+  for (int qi = 0; qi < NQT; ++qi) L[qi].init();
+
+  float qr[NQT == 1 ? VPL * EPV : 1];
+  if constexpr (NQT == 1) {
+#pragma unroll
+    for (int i = 0; i < VPL; ++i)
+#pragma unroll
+      for (int e = 0; e < EPV; ++e) {
+        const int v = j + 16 * i;
+        qr[i * EPV + e] = v < VPR ? q_lds[v * EPV + e] : 0.f;
+      }
+  }
+
+  float cand[NQT];
+#pragma unroll
+  for (int qi = 0; qi < NQT; ++qi) cand[qi] = 0.f;
+
+  for (int base = wb; base < we; base += 64) {
+#pragma unroll 2
+    for (int it = 0; it < 16; ++it) {
+      const int row = base + it * 4 + g;
+      const bool valid = row < we;
+      const uint8_t* rp = X + (int64_t)(valid ? row : wb) * RB;
+      uint4 v[VPL];
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) {
+        const int vv = j + 16 * i;
+        if (16 * i < VPR && vv < VPR)
+          v[i] = *(const uint4*)(rp + (int64_t)vv * 16);
+        else
+          v[i] = make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int qi = 0; qi < NQT; ++qi) {
+        float acc = 0.f;
+#pragma unroll
+        for (int i = 0; i < VPL; ++i) {
+          if (16 * i >= VPR) continue;
+#pragma unroll
+          for (int e = 0; e < EPV; ++e) {
+            float qv;
+            if constexpr (NQT == 1)
+              qv = qr[i * EPV + e];
+            else
+              qv = (j + 16 * i < VPR) ? q_lds[qi * D + (j + 16 * i) * EPV + e] : 0.f;
+            acc = fmaf(elem<DT>(v[i], e), qv, acc);
+          }
+        }
+        acc = row16_sum(acc);
+        if (j == it) cand[qi] = acc;
+      }
+    }
+    const int crow = base + j * 4 + g;
+#pragma unroll
+    for (int qi = 0; qi < NQT; ++qi) L[qi].offer(cand[qi], crow, crow < we);
+  }
+
+  if (lane < K) {
+#pragma unroll
+    for (int qi = 0; qi < NQT; ++qi) {
+      if (qi < nqt) {
+        const int64_t o = ((int64_t)(q0 + qi) * n_lists + wave_g) * K + lane;
+        cand_s[o] = L[qi].ls;
+        cand_r[o] = L[qi].lr;
+      }
+    }
+  }
+}
+
+// K values instantiated for the scan; runtime k is rounded up to one of these and only the
+// first k entries of each list are used by the merge (lists are sorted).
+#define RFX_VALU_K_LIST(X_) X_(4) X_(16) X_(64)
+
+template <int DT, int NQT, int K>
+static int launch_valu_vpl(int vpl, dim3 grid, size_t lds, hipStream_t st, const uint8_t* X, int nrows,
+                           int D, const float* Qf, int nq, int rpw, float* cs, int* cr, int n_lists) {
+#define RFX_L(V)                                                                                  \
+  if (vpl <= V) {                                                                                 \
+    hipLaunchKernelGGL((scan_valu_kernel<DT, NQT, K, V>), grid, dim3(256), lds, st, X, nrows, D, Qf, \
+                       nq, rpw, cs, cr, n_lists);                                                 \
+    return 0;                                                                                     \
+  }
+  RFX_L(4) RFX_L(8) RFX_L(12) RFX_L(16)
+#undef RFX_L
+  return -1;
+}
+
+template <int DT, int NQT>
+static int launch_valu_k(int kk, int vpl, dim3 grid, size_t lds, hipStream_t st, const uint8_t* X,
+                         int nrows, int D, const float* Qf, int nq, int rpw, float* cs, int* cr,
+                         int n_lists) {
+#define RFX_K(KV) \
+  if (kk == KV) return launch_valu_vpl<DT, NQT, KV>(vpl, grid, lds, st, X, nrows, D, Qf, nq, rpw, cs, cr, n_lists);
+  RFX_VALU_K_LIST(RFX_K)
+#undef RFX_K
+  return -1;
+}
+
+int valu_k_slot(int k) { return k <= 4 ? 4 : (k <= 16 ? 16 : 64); }
+
+ValuPlan plan_scan_valu(int64_t nrows, int D, int dtype, int64_t nq, int k) {
+  ValuPlan p{};
+  const int esz = dtype == RFX_F32 ? 4 : 2;
+  p.vpr = (int)((int64_t)D * esz / 16);
+  p.vpl = (p.vpr + 15) / 16;
+  p.k_slot = valu_k_slot(k);
+  p.nqt = nq <= 1 ? 1 : (nq <= 4 ? 4 : 8);
+  p.q_slices = (int)((nq + p.nqt - 1) / p.nqt);
+  const int64_t target_waves = 4096;
+  int64_t rpw = (nrows + target_waves - 1) / target_waves;
+  if (rpw < 64) rpw = 64;
+  rpw = (rpw + 63) / 64 * 64;
+  int64_t waves = (nrows + rpw - 1) / rpw;
+  if (waves < 1) waves = 1;
+  p.rows_per_wave = (int)rpw;
+  p.blocks = (int)((waves + 3) / 4);
+  p.n_lists = p.blocks * 4;
+  p.ok = p.vpl <= 16 && p.k_slot <= 64 && (int64_t)D * esz % 16 == 0;
+  return p;
+}
+
+int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dtype, const float* Qf,
+                     int nq, float* cs, int* cr, hipStream_t st) {
+  dim3 grid(p.blocks, p.q_slices);
+  const size_t lds = (size_t)p.nqt * D * sizeof(float);
+  const uint8_t* Xb = (const uint8_t*)X;
+#define RFX_NQ(NQV)                                                                                \
+  if (p.nqt == NQV) {                                                                              \
+    if (dtype == RFX_F32)                                                                          \
+      return launch_valu_k<RFX_F32, NQV>(p.k_slot, p.vpl, grid, lds, st, Xb, nrows, D, Qf, nq,       \
+                                         p.rows_per_wave, cs, cr, p.n_lists);                      \
+    if (dtype == RFX_BF16)                                                                         \
+      return launch_valu_k<RFX_BF16, NQV>(p.k_slot, p.vpl, grid, lds, st, Xb, nrows, D, Qf, nq,      \
+                                          p.rows_per_wave, cs, cr, p.n_lists);                     \
+    return launch_valu_k<RFX_F16, NQV>(p.k_slot, p.vpl, grid, lds, st, Xb, nrows, D, Qf, nq,         \
+                                       p.rows_per_wave, cs, cr, p.n_lists);                        \
+  }
+  RFX_NQ(1) RFX_NQ(4) RFX_NQ(8)
+#undef RFX_NQ
+  return -1;
+}
+
+// Widen index-dtype queries to f32 (exact).
+__global__ void widen_queries_kernel(const void* __restrict__ Q, int64_t n, int dtype, float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (dtype == RFX_F32)
+      out[i] = ((const float*)Q)[i];
+    else if (dtype == RFX_BF16)
+      out[i] = bf16_to_f32(((const uint16_t*)Q)[i]);
+    else
+      out[i] = f16_to_f32(((const uint16_t*)Q)[i]);
+  }
+}
+
+void launch_widen_queries(const void* Q, int64_t n, int dtype, float* out, hipStream_t st) {
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(widen_queries_kernel, dim3(blocks < 1 ? 1 : blocks), dim3(256), 0, st, Q, n, dtype, out);
+}
+
+// ---------------------------------------------------------------------------------------
+// Top-k merge: one 512-thread block per query; each wave folds a strided share of the
+// candidates into a wave list, then wave 0 folds the other 7 lists (through LDS).
+// Candidates: [nq][n_cand] (score, row) with rows int32 (local) or int64 (global).
+// ---------------------------------------------------------------------------------------
+template <int K, bool R64>
+__global__ __launch_bounds__(512) void merge_kernel(const float* __restrict__ cs, const void* __restrict__ cr,
+                                                    int64_t n_cand, int k_out, int64_t row_offset,
+                                                    float* __restrict__ out_s, int64_t* __restrict__ out_r) {
+  __shared__ float ls_lds[8][K];
+  __shared__ long long lr_lds[8][K];
+  const int q = blockIdx.x;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const float* s = cs + (int64_t)q * n_cand;
+  WaveList64<K> L;
+  L.init();
+  for (int64_t b = (int64_t)w * 64; b < n_cand; b += 8 * 64) {
+    const int64_t i = b + lane;
+    const bool valid = i < n_cand;
+    float sc = valid ? s[i] : -__builtin_inff();
+    long long rr;
+    if constexpr (R64)
+      rr = valid ? ((const long long*)cr)[(int64_t)q * n_cand + i] : 0x7fffffffffffffffll;
+    else
+      rr = valid ? (long long)((const int*)cr)[(int64_t)q * n_cand + i] : 0x7fffffffffffffffll;
+    // empty slots of partial lists carry the sentinel row: never valid candidates
+    const bool live = valid && rr >= 0 && rr != 0x7fffffffffffffffll && (R64 || rr != (long long)kEmptyRow);
+    L.offer(sc, rr, live);
+  }
+  if (lane < K) {
+    ls_lds[w][lane] = L.ls;
+    lr_lds[w][lane] = L.lr;
+  }
+  __syncthreads();
+  if (w == 0) {
+    for (int ww = 1; ww < 8; ++ww) {
+      const bool valid = lane < K;
+      const float sc = valid ? ls_lds[ww][lane] : -__builtin_inff();
+      const long long rr = valid ? lr_lds[ww][lane] : 0x7fffffffffffffffll;
+      L.offer(sc, rr, valid && rr != 0x7fffffffffffffffll);
+    }
+    if (lane < k_out) {
+      const bool empty = L.lr == 0x7fffffffffffffffll;
+      out_s[(int64_t)q * k_out + lane] = empty ? -__builtin_inff() : L.ls;
+      out_r[(int64_t)q * k_out + lane] = empty ? -1 : L.lr + row_offset;
+    }
+  }
+}
+
+int launch_topk_merge(const float* cs, const void* cr, int rows_are_i64, int64_t nq, int64_t n_cand, int k,
+                      int64_t row_offset, float* out_s, int64_t* out_r, hipStream_t st) {
+  const int kk = valu_k_slot(k);
+  if (nq <= 0) return 0;
+#define RFX_M(KV)                                                                                  \
+  if (kk == KV) {                                                                                  \
+    if (rows_are_i64)                                                                              \
+      hipLaunchKernelGGL((merge_kernel<KV, true>), dim3((unsigned)nq), dim3(512), 0, st, cs, cr,    \
+                         n_cand, k, row_offset, out_s, out_r);                                     \
+    else                                                                                           \
+      hipLaunchKernelGGL((merge_kernel<KV, false>), dim3((unsigned)nq), dim3(512), 0, st, cs, cr,   \
+                         n_cand, k, row_offset, out_s, out_r);                                     \
+    return 0;                                                                                      \
+  }
+  RFX_VALU_K_LIST(RFX_M)
+#undef RFX_M
+  return -1;
+}
+
+}  // namespace rfx

@@ -1,0 +1,521 @@
+// rfx_api.hip — C-ABI of librfx (declared in include/rfx.h).
+//
+// Owns the vector-store storage (one device buffer per index handle) and dispatches the
+// kernels.  Everything else (queries, outputs, workspaces) is caller-owned device memory —
+// in practice torch tensors allocated by the Python host (rag-foundation_amd/rfx).
+//
+// Thread-safety: handles live in a process-wide registry; each index has a reader/writer
+// lock (search = shared, add/tombstone/reserve = exclusive), matching the concurrency the
+// reference's callers generate (<=50 chat threads per process, chat.py:496-521; <=10 ingestion
+// jobs per worker, worker.py:125).
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
+#include <vector>
+
+#include "rfx_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define RFX_HIP(call)                                                                          \
+  do {                                                                                         \
+    hipError_t e_ = (call);                                                                    \
+    if (e_ != hipSuccess) return fail(RFX_EDEVICE, "%s: %s", #call, hipGetErrorString(e_));    \
+  } while (0)
+
+int esize(int dtype) { return dtype == RFX_F32 ? 4 : 2; }
+bool valid_dtype(int dtype) { return dtype == RFX_F32 || dtype == RFX_BF16 || dtype == RFX_F16; }
+
+struct Index {
+  int device = 0;
+  int dim = 0;
+  int dtype = 0;
+  int64_t rows = 0;
+  int64_t capacity = 0;
+  int64_t live = 0;
+  void* data = nullptr;
+  std::vector<uint8_t> tomb;  // host bitmap (1 = deleted), mirrors the NaN rows on device
+  std::shared_mutex mu;
+  int64_t row_bytes() const { return (int64_t)dim * esize(dtype); }
+};
+
+std::mutex g_reg_mu;
+std::map<uint64_t, std::shared_ptr<Index>> g_reg;
+std::atomic<uint64_t> g_next{1};
+
+std::shared_ptr<Index> get(rfx_index_t h) {
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  auto it = g_reg.find(h);
+  return it == g_reg.end() ? nullptr : it->second;
+}
+
+int grow(Index& ix, int64_t need, hipStream_t st) {
+  if (need <= ix.capacity) return RFX_OK;
+  int64_t cap = ix.capacity > 0 ? ix.capacity : 1024;
+  while (cap < need) cap = cap + cap / 2 + 1024;
+  cap = (cap + 127) / 128 * 128;  // whole 128-row scan tiles
+  void* p = nullptr;
+  const size_t bytes = (size_t)cap * ix.row_bytes();
+  if (hipMalloc(&p, bytes) != hipSuccess) return fail(RFX_ENOMEM, "hipMalloc(%zu) failed for index", bytes);
+  if (ix.rows > 0) {
+    RFX_HIP(hipMemcpyAsync(p, ix.data, (size_t)ix.rows * ix.row_bytes(), hipMemcpyDeviceToDevice, st));
+    RFX_HIP(hipStreamSynchronize(st));
+  }
+  if (ix.data) RFX_HIP(hipFree(ix.data));  // hipFree waits for in-flight work on the old buffer
+  ix.data = p;
+  ix.capacity = cap;
+  return RFX_OK;
+}
+
+// ---- search workspace layout ------------------------------------------------------------------
+struct SearchLayout {
+  int kernel;        // 0 = VALU, 1 = MFMA
+  rfx::ValuPlan vp;
+  rfx::MfmaPlan mp;
+  int64_t n_cand;    // candidates per query
+  size_t q_off, q_bytes, cs_off, cr_off, total;
+};
+
+size_t align_up(size_t x) { return (x + 255) / 256 * 256; }
+
+int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
+  if (k < 1 || k > 64) return fail(RFX_EINVAL, "k=%d out of range [1, 64]", k);
+  if (nq < 0) return fail(RFX_EINVAL, "nq < 0");
+  if (ix.rows >= (int64_t)INT32_MAX) return fail(RFX_EUNSUPPORTED, "shard exceeds 2^31-1 rows");
+  L = SearchLayout{};
+  L.mp = rfx::plan_scan_mfma(ix.rows, ix.dim, ix.dtype, nq, k);
+  L.vp = rfx::plan_scan_valu(ix.rows, ix.dim, ix.dtype, nq, k);
+  const bool use_mfma = L.mp.ok && nq > 8;
+  L.kernel = use_mfma ? 1 : 0;
+  if (use_mfma) {
+    L.n_cand = L.mp.n_lists * L.mp.k_lane;
+    L.q_bytes = (size_t)L.mp.nq_pad * ix.dim * 2;
+  } else {
+    if (!L.vp.ok) return fail(RFX_EUNSUPPORTED, "no scan kernel for dim=%d dtype=%d k=%d", ix.dim, ix.dtype, k);
+    L.n_cand = (int64_t)L.vp.n_lists * L.vp.k_slot;
+    L.q_bytes = (size_t)nq * ix.dim * 4;
+  }
+  if (ix.rows == 0) L.n_cand = 0;
+  L.q_off = 0;
+  L.cs_off = align_up(L.q_bytes);
+  L.cr_off = L.cs_off + align_up((size_t)nq * L.n_cand * 4);
+  L.total = L.cr_off + align_up((size_t)nq * L.n_cand * 4);
+  return RFX_OK;
+}
+
+int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq, float* cs, int32_t* cr,
+              uint8_t* ws, hipStream_t st) {
+  if (ix.rows == 0 || nq == 0) return RFX_OK;
+  if (L.kernel == 1) {
+    void* qpad = ws + L.q_off;
+    rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, 2, qpad, st);
+    if (rfx::launch_scan_mfma(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, cs, cr, st) != 0)
+      return fail(RFX_EUNSUPPORTED, "MFMA scan launch rejected");
+  } else {
+    float* qf = (float*)(ws + L.q_off);
+    rfx::launch_widen_queries(queries, nq * ix.dim, ix.dtype, qf, st);
+    if (rfx::launch_scan_valu(L.vp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qf, (int)nq, cs, cr, st) != 0)
+      return fail(RFX_EUNSUPPORTED, "VALU scan launch rejected");
+  }
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rfx_last_error(void) { return g_err.c_str(); }
+
+int rfx_version(void) { return 100; }
+
+int rfx_device_count(int* out_n) {
+  if (!out_n) return fail(RFX_EINVAL, "null out");
+  int n = 0;
+  RFX_HIP(hipGetDeviceCount(&n));
+  *out_n = n;
+  return RFX_OK;
+}
+
+int rfx_init(int device) {
+  RFX_HIP(hipSetDevice(device));
+  return RFX_OK;
+}
+
+int rfx_index_create(int device, int dim, int dtype, int64_t capacity, rfx_index_t* out) {
+  if (!out) return fail(RFX_EINVAL, "null out");
+  if (dim <= 0 || dim % 64 != 0 || dim > 4096) return fail(RFX_EINVAL, "dim=%d must be a positive multiple of 64 <= 4096", dim);
+  if (!valid_dtype(dtype)) return fail(RFX_EINVAL, "bad dtype %d", dtype);
+  if (capacity < 0) return fail(RFX_EINVAL, "capacity < 0");
+  RFX_HIP(hipSetDevice(device));
+  auto ix = std::make_shared<Index>();
+  ix->device = device;
+  ix->dim = dim;
+  ix->dtype = dtype;
+  if (capacity > 0) {
+    int rc = grow(*ix, capacity, nullptr);
+    if (rc) return rc;
+  }
+  const uint64_t h = g_next++;
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg[h] = ix;
+  }
+  *out = h;
+  return RFX_OK;
+}
+
+int rfx_index_destroy(rfx_index_t h) {
+  std::shared_ptr<Index> ix;
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg.find(h);
+    if (it == g_reg.end()) return fail(RFX_EINVAL, "unknown index handle %llu", (unsigned long long)h);
+    ix = it->second;
+    g_reg.erase(it);
+  }
+  std::unique_lock<std::shared_mutex> lk(ix->mu);
+  if (ix->data) {
+    RFX_HIP(hipSetDevice(ix->device));
+    RFX_HIP(hipFree(ix->data));
+    ix->data = nullptr;
+  }
+  return RFX_OK;
+}
+
+int rfx_index_info(rfx_index_t h, int* dim, int* dtype, int64_t* rows, int64_t* capacity, int64_t* live_rows) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  if (dim) *dim = ix->dim;
+  if (dtype) *dtype = ix->dtype;
+  if (rows) *rows = ix->rows;
+  if (capacity) *capacity = ix->capacity;
+  if (live_rows) *live_rows = ix->live;
+  return RFX_OK;
+}
+
+int rfx_index_reserve(rfx_index_t h, int64_t capacity) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  std::unique_lock<std::shared_mutex> lk(ix->mu);
+  RFX_HIP(hipSetDevice(ix->device));
+  return grow(*ix, capacity, nullptr);
+}
+
+int rfx_index_add(rfx_index_t h, const void* vecs, int64_t n, int src_is_device, int64_t* out_first_row, void* stream) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  if (n < 0 || (n > 0 && !vecs)) return fail(RFX_EINVAL, "bad vectors");
+  hipStream_t st = (hipStream_t)stream;
+  std::unique_lock<std::shared_mutex> lk(ix->mu);
+  RFX_HIP(hipSetDevice(ix->device));
+  int rc = grow(*ix, ix->rows + n, st);
+  if (rc) return rc;
+  const int64_t first = ix->rows;
+  if (n > 0) {
+    RFX_HIP(hipMemcpyAsync((uint8_t*)ix->data + first * ix->row_bytes(), vecs, (size_t)n * ix->row_bytes(),
+                           src_is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+    if (!src_is_device) RFX_HIP(hipStreamSynchronize(st));  // host buffer may be freed on return
+  }
+  ix->rows += n;
+  ix->live += n;
+  ix->tomb.resize((size_t)(ix->rows + 7) / 8, 0);
+  if (out_first_row) *out_first_row = first;
+  return RFX_OK;
+}
+
+int rfx_index_add_synthetic(rfx_index_t h, uint64_t seed, int64_t gen_row0, int64_t n, int64_t* out_first_row,
+                            void* stream) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  if (n < 0) return fail(RFX_EINVAL, "n < 0");
+  hipStream_t st = (hipStream_t)stream;
+  std::unique_lock<std::shared_mutex> lk(ix->mu);
+  RFX_HIP(hipSetDevice(ix->device));
+  int rc = grow(*ix, ix->rows + n, st);
+  if (rc) return rc;
+  const int64_t first = ix->rows;
+  if (n > 0) {
+    rfx::launch_synth_rows(seed, gen_row0 < 0 ? first : gen_row0, n, ix->dim, ix->dtype,
+                           (uint8_t*)ix->data + first * ix->row_bytes(), st);
+    RFX_HIP(hipGetLastError());
+  }
+  ix->rows += n;
+  ix->live += n;
+  ix->tomb.resize((size_t)(ix->rows + 7) / 8, 0);
+  if (out_first_row) *out_first_row = first;
+  return RFX_OK;
+}
+
+int rfx_index_tombstone(rfx_index_t h, const int64_t* rows_h, int64_t n, void* stream) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  if (n < 0 || (n > 0 && !rows_h)) return fail(RFX_EINVAL, "bad rows");
+  hipStream_t st = (hipStream_t)stream;
+  std::unique_lock<std::shared_mutex> lk(ix->mu);
+  std::vector<int64_t> todo;
+  todo.reserve((size_t)n);
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t r = rows_h[i];
+    if (r < 0 || r >= ix->rows) return fail(RFX_EINVAL, "row %lld out of range", (long long)r);
+    uint8_t& b = ix->tomb[(size_t)r >> 3];
+    if (!(b & (1u << (r & 7)))) {
+      b |= (uint8_t)(1u << (r & 7));
+      todo.push_back(r);
+    }
+  }
+  if (todo.empty()) return RFX_OK;
+  RFX_HIP(hipSetDevice(ix->device));
+  int64_t* d = nullptr;
+  RFX_HIP(hipMalloc(&d, todo.size() * sizeof(int64_t)));
+  RFX_HIP(hipMemcpyAsync(d, todo.data(), todo.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
+  rfx::launch_nan_rows(ix->data, d, (int64_t)todo.size(), ix->row_bytes(), ix->dtype, st);
+  RFX_HIP(hipGetLastError());
+  RFX_HIP(hipStreamSynchronize(st));
+  RFX_HIP(hipFree(d));
+  ix->live -= (int64_t)todo.size();
+  return RFX_OK;
+}
+
+int rfx_index_read(rfx_index_t h, int64_t row0, int64_t n, void* dst, int dst_is_device, void* stream) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  if (row0 < 0 || n < 0 || row0 + n > ix->rows) return fail(RFX_EINVAL, "rows [%lld, %lld) out of range", (long long)row0, (long long)(row0 + n));
+  if (n == 0) return RFX_OK;
+  if (!dst) return fail(RFX_EINVAL, "null destination");
+  RFX_HIP(hipSetDevice(ix->device));
+  hipStream_t st = (hipStream_t)stream;
+  RFX_HIP(hipMemcpyAsync(dst, (uint8_t*)ix->data + row0 * ix->row_bytes(), (size_t)n * ix->row_bytes(),
+                         dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, st));
+  if (!dst_is_device) RFX_HIP(hipStreamSynchronize(st));
+  return RFX_OK;
+}
+
+int rfx_index_data(rfx_index_t h, void** out_ptr) {
+  auto ix = get(h);
+  if (!ix || !out_ptr) return fail(RFX_EINVAL, "unknown index handle / null out");
+  *out_ptr = ix->data;
+  return RFX_OK;
+}
+
+// File format (little endian): "RFXIDX01" | u32 version=1 | u32 dim | u32 dtype | u32 0 |
+// i64 rows | i64 live | tombstone bitmap ceil(rows/8) B | rows*dim*esize B of row data.
+int rfx_index_save(rfx_index_t h, const char* path) {
+  auto ix = get(h);
+  if (!ix || !path) return fail(RFX_EINVAL, "unknown index handle / null path");
+  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  RFX_HIP(hipSetDevice(ix->device));
+  const std::string tmp = std::string(path) + ".tmp";
+  FILE* f = fopen(tmp.c_str(), "wb");
+  if (!f) return fail(RFX_EIO, "cannot open %s", tmp.c_str());
+  const uint32_t hdr[4] = {1u, (uint32_t)ix->dim, (uint32_t)ix->dtype, 0u};
+  const int64_t cnt[2] = {ix->rows, ix->live};
+  bool ok = fwrite("RFXIDX01", 1, 8, f) == 8 && fwrite(hdr, 4, 4, f) == 4 && fwrite(cnt, 8, 2, f) == 2;
+  const size_t tb = (size_t)(ix->rows + 7) / 8;
+  if (ok && tb) ok = fwrite(ix->tomb.data(), 1, tb, f) == tb;
+  const size_t total = (size_t)ix->rows * ix->row_bytes();
+  std::vector<uint8_t> buf;
+  const size_t chunk = (size_t)256 << 20;
+  for (size_t off = 0; ok && off < total; off += chunk) {
+    const size_t nb = std::min(chunk, total - off);
+    buf.resize(nb);
+    if (hipMemcpy(buf.data(), (uint8_t*)ix->data + off, nb, hipMemcpyDeviceToHost) != hipSuccess) {
+      fclose(f);
+      return fail(RFX_EDEVICE, "hipMemcpy D2H failed while saving");
+    }
+    ok = fwrite(buf.data(), 1, nb, f) == nb;
+  }
+  ok = (fclose(f) == 0) && ok;
+  if (!ok) return fail(RFX_EIO, "write failed for %s", tmp.c_str());
+  if (rename(tmp.c_str(), path) != 0) return fail(RFX_EIO, "rename to %s failed", path);
+  return RFX_OK;
+}
+
+int rfx_index_load(const char* path, int device, rfx_index_t* out) {
+  if (!path || !out) return fail(RFX_EINVAL, "null path / out");
+  FILE* f = fopen(path, "rb");
+  if (!f) return fail(RFX_EIO, "cannot open %s", path);
+  char magic[8];
+  uint32_t hdr[4];
+  int64_t cnt[2];
+  if (fread(magic, 1, 8, f) != 8 || memcmp(magic, "RFXIDX01", 8) != 0 || fread(hdr, 4, 4, f) != 4 ||
+      fread(cnt, 8, 2, f) != 2 || hdr[0] != 1u) {
+    fclose(f);
+    return fail(RFX_EIO, "%s is not an rfx index file", path);
+  }
+  rfx_index_t h = 0;
+  int rc = rfx_index_create(device, (int)hdr[1], (int)hdr[2], cnt[0], &h);
+  if (rc) {
+    fclose(f);
+    return rc;
+  }
+  auto ix = get(h);
+  const size_t tb = (size_t)(cnt[0] + 7) / 8;
+  ix->tomb.assign(tb, 0);
+  if (tb && fread(ix->tomb.data(), 1, tb, f) != tb) {
+    fclose(f);
+    rfx_index_destroy(h);
+    return fail(RFX_EIO, "truncated tombstones in %s", path);
+  }
+  const size_t total = (size_t)cnt[0] * ix->row_bytes();
+  std::vector<uint8_t> buf;
+  const size_t chunk = (size_t)256 << 20;
+  for (size_t off = 0; off < total; off += chunk) {
+    const size_t nb = std::min(chunk, total - off);
+    buf.resize(nb);
+    if (fread(buf.data(), 1, nb, f) != nb) {
+      fclose(f);
+      rfx_index_destroy(h);
+      return fail(RFX_EIO, "truncated rows in %s", path);
+    }
+    if (hipMemcpy((uint8_t*)ix->data + off, buf.data(), nb, hipMemcpyHostToDevice) != hipSuccess) {
+      fclose(f);
+      rfx_index_destroy(h);
+      return fail(RFX_EDEVICE, "hipMemcpy H2D failed while loading");
+    }
+  }
+  fclose(f);
+  ix->rows = cnt[0];
+  ix->live = cnt[1];
+  *out = h;
+  return RFX_OK;
+}
+
+// ---- search ---------------------------------------------------------------------------------------
+int rfx_search_workspace_bytes(rfx_index_t h, int64_t nq, int k, size_t* out_bytes) {
+  auto ix = get(h);
+  if (!ix || !out_bytes) return fail(RFX_EINVAL, "unknown index handle / null out");
+  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  SearchLayout L;
+  int rc = make_layout(*ix, nq, k, L);
+  if (rc) return rc;
+  *out_bytes = L.total;
+  return RFX_OK;
+}
+
+int rfx_scan_plan(rfx_index_t h, int64_t nq, int k, int* out_kernel, int64_t* out_n_cand) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  SearchLayout L;
+  int rc = make_layout(*ix, nq, k, L);
+  if (rc) return rc;
+  if (out_kernel) *out_kernel = L.kernel;
+  if (out_n_cand) *out_n_cand = L.n_cand;
+  return RFX_OK;
+}
+
+int rfx_scan_topk(rfx_index_t h, const void* queries_d, int64_t nq, int k, float* cand_scores_d,
+                  int32_t* cand_rows_d, void* ws_d, size_t ws_bytes, void* stream) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  SearchLayout L;
+  int rc = make_layout(*ix, nq, k, L);
+  if (rc) return rc;
+  if (ws_bytes < L.q_bytes || (L.q_bytes && !ws_d)) return fail(RFX_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, L.q_bytes);
+  if (nq > 0 && !queries_d) return fail(RFX_EINVAL, "null queries");
+  RFX_HIP(hipSetDevice(ix->device));
+  return scan_into(*ix, L, queries_d, nq, cand_scores_d, cand_rows_d, (uint8_t*)ws_d, (hipStream_t)stream);
+}
+
+int rfx_topk_merge(const float* cand_scores_d, const void* cand_rows_d, int rows_are_i64, int64_t nq, int64_t n_cand,
+                   int k, int64_t row_offset, float* out_scores_d, int64_t* out_rows_d, void* stream) {
+  if (k < 1 || k > 64) return fail(RFX_EINVAL, "k=%d out of range [1, 64]", k);
+  if (nq < 0 || n_cand < 0) return fail(RFX_EINVAL, "negative sizes");
+  if (nq > 0 && (!out_scores_d || !out_rows_d)) return fail(RFX_EINVAL, "null outputs");
+  if (rfx::launch_topk_merge(cand_scores_d, cand_rows_d, rows_are_i64, nq, n_cand, k, row_offset, out_scores_d,
+                             out_rows_d, (hipStream_t)stream) != 0)
+    return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
+int rfx_search(rfx_index_t h, const void* queries_d, int64_t nq, int k, float* out_scores_d, int64_t* out_rows_d,
+               void* ws_d, size_t ws_bytes, void* stream) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  SearchLayout L;
+  int rc = make_layout(*ix, nq, k, L);
+  if (rc) return rc;
+  if (ws_bytes < L.total || (L.total && !ws_d)) return fail(RFX_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, L.total);
+  if (nq > 0 && (!queries_d || !out_scores_d || !out_rows_d)) return fail(RFX_EINVAL, "null queries / outputs");
+  RFX_HIP(hipSetDevice(ix->device));
+  hipStream_t st = (hipStream_t)stream;
+  uint8_t* ws = (uint8_t*)ws_d;
+  float* cs = (float*)(ws + L.cs_off);
+  int32_t* cr = (int32_t*)(ws + L.cr_off);
+  rc = scan_into(*ix, L, queries_d, nq, cs, cr, ws, st);
+  if (rc) return rc;
+  if (rfx::launch_topk_merge(cs, cr, 0, nq, L.n_cand, k, 0, out_scores_d, out_rows_d, st) != 0)
+    return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
+// ---- embedding -------------------------------------------------------------------------------------
+int rfx_embed_weights(int V, int dim, uint64_t seed, void* wt_d, void* stream) {
+  if (V <= 0 || (V & (V - 1)) || V % 16 != 0) return fail(RFX_EINVAL, "V=%d must be a power of two >= 16", V);
+  if (dim <= 0 || dim % 32 != 0 || dim > 1024) return fail(RFX_EINVAL, "dim=%d must be a multiple of 32 <= 1024", dim);
+  if (!wt_d) return fail(RFX_EINVAL, "null weights");
+  rfx::launch_embed_weights(V, dim, seed, wt_d, (hipStream_t)stream);
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
+int rfx_embed_workspace_bytes(int64_t n, int V, size_t* out_bytes) {
+  if (!out_bytes || n < 0 || V <= 0) return fail(RFX_EINVAL, "bad arguments");
+  *out_bytes = align_up((size_t)n * V * 2);
+  return RFX_OK;
+}
+
+int rfx_embed(const int32_t* indptr_d, const int32_t* bucket_d, const int16_t* count_d, int64_t n, int V,
+              const void* wt_d, int dim, void* out_d, int out_dtype, void* ws_d, size_t ws_bytes, void* stream) {
+  if (n < 0) return fail(RFX_EINVAL, "n < 0");
+  if (V <= 0 || (V & (V - 1)) || V % 16 != 0) return fail(RFX_EINVAL, "V=%d must be a power of two >= 16", V);
+  if (dim <= 0 || dim % 32 != 0 || dim > 1024) return fail(RFX_EINVAL, "dim=%d must be a multiple of 32 <= 1024", dim);
+  if (!valid_dtype(out_dtype)) return fail(RFX_EINVAL, "bad dtype %d", out_dtype);
+  if (n == 0) return RFX_OK;
+  if (!indptr_d || !bucket_d || !count_d || !wt_d || !out_d) return fail(RFX_EINVAL, "null pointer argument");
+  if (ws_bytes < (size_t)n * V * 2) return fail(RFX_EINVAL, "embed workspace too small");
+  int rc = rfx::launch_embed(indptr_d, bucket_d, count_d, n, V, wt_d, dim, out_d, out_dtype, ws_d, (hipStream_t)stream);
+  if (rc == -2) return fail(RFX_EDEVICE, "hipMemsetAsync failed");
+  if (rc) return fail(RFX_EUNSUPPORTED, "embed dim=%d unsupported", dim);
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
+int rfx_synth_rows(uint64_t seed, int64_t row0, int64_t n, int dim, int dtype, void* out_d, void* stream) {
+  if (n < 0 || row0 < 0 || dim <= 0 || !valid_dtype(dtype)) return fail(RFX_EINVAL, "bad arguments");
+  if (n == 0) return RFX_OK;
+  if (!out_d) return fail(RFX_EINVAL, "null output");
+  rfx::launch_synth_rows(seed, row0, n, dim, dtype, out_d, (hipStream_t)stream);
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,155 @@
+// rfx_device.h — device-side helpers shared by the gfx950 kernels.
+// CDNA4 only: wave64, DPP row ops, MFMA builtins.  No CUDA-compat layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rfx {
+
+constexpr int kWave = 64;
+constexpr int kEmptyRow = 0x7fffffff;  // internal "no row" sentinel (worst under the tie rule)
+
+// ---- ranking rule: score desc, then row asc -------
+// NaN scores (tombstoned rows) never compare better than anything, so they are never kept.
+__device__ __forceinline__ bool better(float s1, int r1, float s2, int r2) {
+  return s1 > s2 || (s1 == s2 && r1 < r2);
+}
+__device__ __forceinline__ bool better64(float s1, long long r1, float s2, long long r2) {
+  return s1 > s2 || (s1 == s2 && r1 < r2);
+}
+
+// ---- counter-based generator (oracle/synth.py restates this bit-for-bit) ----------------
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// ---- fp32 <-> 16-bit storage -----------------------------------------------------------------
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) {
+  return __uint_as_float(((uint32_t)h) << 16);
+}
+// round-to-nearest-even; NaN stays NaN (quiet)
+__host__ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  uint32_t u;
+  __builtin_memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ float f16_to_f32(uint16_t h) {
+  return (float)__builtin_bit_cast(_Float16, h);
+}
+__device__ __forceinline__ uint16_t f32_to_f16(float f) {
+  return __builtin_bit_cast(uint16_t, (_Float16)f);
+}
+
+// ---- cross-lane -------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ int readlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+// sum over each DPP row of 16 lanes; every lane of the row receives the row sum.
+// row_ror:n (0x120+n) rotates within the 16-lane row.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x122, 0xf, 0xf, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xf, 0xf, false));
+  return v;
+}
+
+// ---- wave-resident top-K list ------------------------------------------------------------------
+// The list lives in lanes 0..K-1 of (ls, lr), best first; empty slots are (-inf, kEmptyRow).
+// Candidates arrive one per lane; those that beat the wave-uniform threshold (entry K-1) are
+// inserted one at a time (ballot + popcount for the position, one shuffle to shift).
+template <int K>
+struct WaveList {
+  float ls;
+  int lr;
+  float ts;  // threshold = entry K-1 (wave-uniform)
+  int tr;
+
+  __device__ __forceinline__ void init() {
+    ls = -__builtin_inff();
+    lr = kEmptyRow;
+    ts = -__builtin_inff();
+    tr = kEmptyRow;
+  }
+
+  __device__ __forceinline__ void offer(float cs, int cr, bool valid) {
+    const int lane = lane_id();
+    uint64_t mask = __ballot(valid && better(cs, cr, ts, tr));
+    while (mask) {
+      const int j = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const float s = readlane_f(cs, j);
+      const int r = readlane_i(cr, j);
+      if (!better(s, r, ts, tr)) continue;  // wave-uniform: threshold may have risen
+      const bool b = (lane < K) && better(ls, lr, s, r);
+      const int pos = __popcll(__ballot(b));
+      const float us = __shfl_up(ls, 1);
+      const int ur = __shfl_up(lr, 1);
+      if (lane > pos && lane < K) {
+        ls = us;
+        lr = ur;
+      }
+      if (lane == pos) {
+        ls = s;
+        lr = r;
+      }
+      ts = readlane_f(ls, K - 1);
+      tr = readlane_i(lr, K - 1);
+    }
+  }
+};
+
+// Same with 64-bit row ids (cross-shard merge of global rows).
+template <int K>
+struct WaveList64 {
+  float ls;
+  long long lr;
+  float ts;
+  long long tr;
+
+  __device__ __forceinline__ void init() {
+    ls = -__builtin_inff();
+    lr = 0x7fffffffffffffffll;
+    ts = -__builtin_inff();
+    tr = 0x7fffffffffffffffll;
+  }
+
+  __device__ __forceinline__ void offer(float cs, long long cr, bool valid) {
+    const int lane = lane_id();
+    uint64_t mask = __ballot(valid && better64(cs, cr, ts, tr));
+    while (mask) {
+      const int j = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const float s = readlane_f(cs, j);
+      const long long r = (long long)(((uint64_t)(uint32_t)readlane_i((int)(cr >> 32), j) << 32) |
+                                      (uint32_t)readlane_i((int)cr, j));
+      if (!better64(s, r, ts, tr)) continue;
+      const bool b = (lane < K) && better64(ls, lr, s, r);
+      const int pos = __popcll(__ballot(b));
+      const float us = __shfl_up(ls, 1);
+      const long long ur = __shfl_up(lr, 1);
+      if (lane > pos && lane < K) {
+        ls = us;
+        lr = ur;
+      }
+      if (lane == pos) {
+        ls = s;
+        lr = r;
+      }
+      ts = readlane_f(ls, K - 1);
+      tr = (long long)(((uint64_t)(uint32_t)readlane_i((int)(lr >> 32), K - 1) << 32) |
+                       (uint32_t)readlane_i((int)lr, K - 1));
+    }
+  }
+};
+
+}  // namespace rfx

@@ -1,0 +1,55 @@
+// rfx_kernels.h — host-side launchers of the gfx950 kernels (called by rfx_api.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <algorithm>
+
+#include "../../include/rfx.h"
+
+namespace rfx {
+
+// ---- generator / maintenance -------------------------------------------------------------
+void launch_synth_rows(uint64_t seed, int64_t row0, int64_t n, int dim, int dtype, void* out,
+                       hipStream_t st);
+void launch_nan_rows(void* X, const int64_t* rows_d, int64_t n, int64_t row_bytes, int dtype,
+                     hipStream_t st);
+void launch_widen_queries(const void* Q, int64_t n, int dtype, float* out, hipStream_t st);
+
+// ---- VALU scan (small nq) ------------------------------------------------------------------
+struct ValuPlan {
+  int vpr, vpl, k_slot, nqt, q_slices, rows_per_wave, blocks, n_lists;
+  bool ok;
+};
+int valu_k_slot(int k);
+ValuPlan plan_scan_valu(int64_t nrows, int D, int dtype, int64_t nq, int k);
+int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dtype, const float* Qf,
+                     int nq, float* cs, int* cr, hipStream_t st);
+
+// ---- MFMA scan (batched bf16 / f16) -------------------------------------------------------
+struct MfmaPlan {
+  int bn;          // queries per workgroup tile (64/128/256)
+  int q_blocks;    // gridDim.y
+  int k_lane;      // lane-list length (>= k)
+  int blocks;      // gridDim.x (persistent over row tiles)
+  int tiles_per_block;
+  int lists_per_block;  // lane lists per query per block
+  int64_t n_lists;      // per query
+  int64_t nq_pad;
+  bool ok;
+};
+MfmaPlan plan_scan_mfma(int64_t nrows, int D, int dtype, int64_t nq, int k);
+int launch_scan_mfma(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad,
+                     int nq, float* cs, int* cr, hipStream_t st);
+void launch_pad_queries(const void* Q, int64_t nq, int64_t nq_pad, int D, int esz, void* out,
+                        hipStream_t st);
+
+// ---- merge -----------------------------------------------------------------------------------
+int launch_topk_merge(const float* cs, const void* cr, int rows_are_i64, int64_t nq, int64_t n_cand,
+                      int k, int64_t row_offset, float* out_s, int64_t* out_r, hipStream_t st);
+
+// ---- embedding ---------------------------------------------------------------------------------
+void launch_embed_weights(int V, int dim, uint64_t seed, void* wt, hipStream_t st);
+int launch_embed(const int32_t* indptr, const int32_t* bucket, const int16_t* count, int64_t n, int V,
+                 const void* wt, int dim, void* out, int out_dtype, void* ws, hipStream_t st);
+
+}  // namespace rfx

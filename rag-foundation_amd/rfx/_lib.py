@@ -1,0 +1,116 @@
+"""ctypes binding of librfx.so (C ABI: include/rfx.h).
+
+torch is imported first on purpose: torch bundles its own libamdhip64.so.7 and librfx.so links
+the same SONAME, so the dynamic loader binds librfx to the runtime torch already loaded — one HIP
+runtime per process, and device pointers / streams from torch are valid inside the library.
+
+There is NO fallback: if librfx.so is missing or fails to load, importing this module raises.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RFX_LIB", os.path.join(_HERE, "librfx.so"))
+
+RFX_OK, RFX_EINVAL, RFX_ENOMEM, RFX_EDEVICE, RFX_EIO, RFX_EBUSY, RFX_EUNSUPPORTED = range(7)
+RFX_F32, RFX_BF16, RFX_F16 = 0, 1, 2
+
+DTYPE_CODES = {"f32": RFX_F32, "bf16": RFX_BF16, "f16": RFX_F16}
+TORCH_DTYPES = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}
+ESIZE = {"f32": 4, "bf16": 2, "f16": 2}
+
+
+class RfxError(RuntimeError):
+    """Non-transient library failure (maps to the reference's fatal-error handling:
+    chat -> SSE unexpected_error frame chat.py:1130-1143; ingestion -> Document ERROR
+    ingestion.py:311-339)."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"rfx error {code}: {msg}")
+        self.code = code
+
+
+class RfxTransientError(TimeoutError):
+    """Transient failure (device busy / queue timeout).  Subclasses TimeoutError so the
+    reference's RETRYABLE_EXCEPTIONS (gemini_rag.py:22-27) retry it unchanged."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"rfx transient error {code}: {msg}")
+        self.code = code
+
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"librfx.so not found at {LIB_PATH}: build it with __graft_entry__.build() "
+                      f"(make -C rag-foundation_amd/csrc); there is no CPU fallback")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+_i = ctypes.c_int
+_i64 = ctypes.c_int64
+_u64 = ctypes.c_uint64
+_p = ctypes.c_void_p
+_sz = ctypes.c_size_t
+_pi = ctypes.POINTER(ctypes.c_int)
+_pi64 = ctypes.POINTER(ctypes.c_int64)
+_pu64 = ctypes.POINTER(ctypes.c_uint64)
+_psz = ctypes.POINTER(ctypes.c_size_t)
+_pp = ctypes.POINTER(ctypes.c_void_p)
+_cs = ctypes.c_char_p
+
+SIGNATURES = {
+    "rfx_last_error": ([], ctypes.c_char_p),
+    "rfx_version": ([], _i),
+    "rfx_device_count": ([_pi], _i),
+    "rfx_init": ([_i], _i),
+    "rfx_index_create": ([_i, _i, _i, _i64, _pu64], _i),
+    "rfx_index_destroy": ([_u64], _i),
+    "rfx_index_info": ([_u64, _pi, _pi, _pi64, _pi64, _pi64], _i),
+    "rfx_index_reserve": ([_u64, _i64], _i),
+    "rfx_index_add": ([_u64, _p, _i64, _i, _pi64, _p], _i),
+    "rfx_index_add_synthetic": ([_u64, _u64, _i64, _i64, _pi64, _p], _i),
+    "rfx_index_tombstone": ([_u64, _pi64, _i64, _p], _i),
+    "rfx_index_read": ([_u64, _i64, _i64, _p, _i, _p], _i),
+    "rfx_index_data": ([_u64, _pp], _i),
+    "rfx_index_save": ([_u64, _cs], _i),
+    "rfx_index_load": ([_cs, _i, _pu64], _i),
+    "rfx_search_workspace_bytes": ([_u64, _i64, _i, _psz], _i),
+    "rfx_search": ([_u64, _p, _i64, _i, _p, _p, _p, _sz, _p], _i),
+    "rfx_scan_plan": ([_u64, _i64, _i, _pi, _pi64], _i),
+    "rfx_scan_topk": ([_u64, _p, _i64, _i, _p, _p, _p, _sz, _p], _i),
+    "rfx_topk_merge": ([_p, _p, _i, _i64, _i64, _i, _i64, _p, _p, _p], _i),
+    "rfx_chunk_whitespace": ([_p, _i64, _i, _i, _p, _i64, _pi64], _i),
+    "rfx_featurize": ([_p, _p, _i64, _i, _u64, _p, _p, _p, _i64, _pi64], _i),
+    "rfx_embed_weights": ([_i, _i, _u64, _p, _p], _i),
+    "rfx_embed_workspace_bytes": ([_i64, _i, _psz], _i),
+    "rfx_embed": ([_p, _p, _p, _i64, _i, _p, _i, _p, _i, _p, _sz, _p], _i),
+    "rfx_synth_rows": ([_u64, _i64, _i64, _i, _i, _p, _p], _i),
+}
+
+for _name, (_args, _res) in SIGNATURES.items():
+    _f = getattr(lib, _name)  # AttributeError here = the library does not export a declared symbol
+    _f.argtypes = _args
+    _f.restype = _res
+
+
+def check(rc: int, what: str = ""):
+    """Raise on a non-zero status code."""
+    if rc == RFX_OK:
+        return
+    msg = lib.rfx_last_error().decode(errors="replace") or what
+    if rc == RFX_EBUSY:
+        raise RfxTransientError(rc, msg)
+    if rc == RFX_EINVAL:
+        raise ValueError(f"rfx: {msg}")
+    raise RfxError(rc, msg)
+
+
+def stream_ptr(stream=None):
+    """hipStream_t of a torch stream (default: the current stream of the current device)."""
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def ptr(t: torch.Tensor):
+    return ctypes.c_void_p(t.data_ptr())

@@ -1,0 +1,63 @@
+"""Row-sharded multi-GPU search: one process per GPU, torch.distributed (backend "nccl" = RCCL
+over xGMI on ROCm).
+
+Partition: rank r owns global rows [offset_r, offset_r + n_r) (contiguous ranges, as even as
+possible).  Per batch every rank (1) scans its shard into a local top-k, (2) adds its row offset,
+(3) all-gathers the packed (score, row) lists — nq·k·16 B per rank, latency-bound on xGMI —
+and (4) merges the world_size·k candidates per query with the same ranking rule.  This is the
+only collective on the path; the reference has none.
+"""
+import torch
+import torch.distributed as dist
+
+
+def shard_range(n_rows: int, rank: int, world: int):
+    """[start, end) of rank's contiguous share of n_rows."""
+    base, extra = divmod(n_rows, world)
+    start = rank * base + min(rank, extra)
+    return start, start + base + (1 if rank < extra else 0)
+
+
+def pack(scores: torch.Tensor, rows: torch.Tensor) -> torch.Tensor:
+    """[nq][k] f32 scores + int64 rows -> one [nq][k][2] int64 buffer (one collective)."""
+    return torch.stack([scores.contiguous().view(torch.int32).to(torch.int64), rows], dim=-1)
+
+
+def unpack(packed: torch.Tensor):
+    """[world][nq][k][2] -> (scores [nq][world*k] f32, rows [nq][world*k] int64)."""
+    world, nq, k, _ = packed.shape
+    p = packed.permute(1, 0, 2, 3).reshape(nq, world * k, 2)
+    scores = p[..., 0].to(torch.int32).contiguous().view(torch.float32)
+    return scores, p[..., 1].contiguous()
+
+
+def gather_merge(local_s: torch.Tensor, local_r: torch.Tensor, k: int, merge, group=None):
+    """All-gather every rank's local top-k (rows already global) and merge them.
+
+    `merge(cand_scores, cand_rows, k)` is the HIP top-k merge (rfx.index.topk_merge) on the GPU
+    path; the gloo CPU tests pass their own.  Returns the global (scores, rows) on every rank.
+    """
+    world = dist.get_world_size(group)
+    if world == 1:
+        return local_s, local_r
+    mine = pack(local_s, local_r)
+    out = torch.empty((world,) + tuple(mine.shape), dtype=mine.dtype, device=mine.device)
+    dist.all_gather_into_tensor(out, mine, group=group)
+    cs, cr = unpack(out)
+    return merge(cs, cr, k)
+
+
+class ShardedSearch:
+    """Holds this rank's DeviceIndex shard and runs the global search."""
+
+    def __init__(self, index, row_offset: int, group=None):
+        self.index = index
+        self.row_offset = int(row_offset)
+        self.group = group
+
+    def search(self, queries: torch.Tensor, k: int, workspace=None, stream=None):
+        from .index import topk_merge
+
+        s, r = self.index.search(queries, k, workspace=workspace, stream=stream)
+        r = torch.where(r >= 0, r + self.row_offset, r)
+        return gather_merge(s, r, k, topk_merge, self.group)

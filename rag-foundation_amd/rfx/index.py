@@ -1,0 +1,182 @@
+"""DeviceIndex — one vector-store shard resident in HBM (wrapper over an rfx_index_t handle).
+
+This is the vector store behind a File Search store name (GeminiRag.create_store,
+backend/app/services/gemini_rag.py:271-304) and the target of the index write
+(upload_file, gemini_rag.py:307-352) and of retrieval (ask_stream, gemini_rag.py:517-551).
+Layout in HBM: row-major [capacity][dim] of the index dtype (f32 / bf16 / f16).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr, stream_ptr
+
+
+class DeviceIndex:
+    def __init__(self, dim: int, dtype: str = "bf16", device: int = 0, capacity: int = 0, _handle=None):
+        if dtype not in _lib.DTYPE_CODES:
+            raise ValueError(f"dtype must be one of {list(_lib.DTYPE_CODES)}")
+        self.dim = int(dim)
+        self.dtype = dtype
+        self.device = int(device)
+        if _handle is not None:
+            self.handle = _handle
+        else:
+            h = ctypes.c_uint64()
+            check(lib.rfx_index_create(self.device, self.dim, _lib.DTYPE_CODES[dtype], int(capacity), ctypes.byref(h)))
+            self.handle = h.value
+
+    # ---- lifecycle ----------------------------------------------------------------------------
+    @classmethod
+    def load(cls, path: str, device: int = 0) -> "DeviceIndex":
+        h = ctypes.c_uint64()
+        check(lib.rfx_index_load(path.encode(), int(device), ctypes.byref(h)))
+        dim, dt = ctypes.c_int(), ctypes.c_int()
+        check(lib.rfx_index_info(h.value, ctypes.byref(dim), ctypes.byref(dt), None, None, None))
+        name = {v: k for k, v in _lib.DTYPE_CODES.items()}[dt.value]
+        return cls(dim.value, name, device, _handle=h.value)
+
+    def save(self, path: str) -> None:
+        check(lib.rfx_index_save(self.handle, path.encode()))
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            check(lib.rfx_index_destroy(self.handle))
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- info ---------------------------------------------------------------------------------
+    def _info(self):
+        rows, cap, live = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        check(lib.rfx_index_info(self.handle, None, None, ctypes.byref(rows), ctypes.byref(cap), ctypes.byref(live)))
+        return rows.value, cap.value, live.value
+
+    @property
+    def rows(self) -> int:
+        return self._info()[0]
+
+    @property
+    def live_rows(self) -> int:
+        return self._info()[2]
+
+    @property
+    def torch_dtype(self):
+        return _lib.TORCH_DTYPES[self.dtype]
+
+    def _dev(self):
+        return torch.device("cuda", self.device)
+
+    # ---- writes -------------------------------------------------------------------------------
+    def reserve(self, capacity: int) -> None:
+        check(lib.rfx_index_reserve(self.handle, int(capacity)))
+
+    def add(self, vecs: torch.Tensor) -> int:
+        """Append normalised rows [n][dim] of the index dtype (device or host tensor)."""
+        if vecs.dim() != 2 or vecs.shape[1] != self.dim:
+            raise ValueError(f"expected [n][{self.dim}] rows, got {tuple(vecs.shape)}")
+        if vecs.dtype != self.torch_dtype:
+            raise ValueError(f"expected {self.torch_dtype} rows, got {vecs.dtype}")
+        vecs = vecs.contiguous()
+        first = ctypes.c_int64()
+        on_dev = vecs.is_cuda
+        st = stream_ptr(torch.cuda.current_stream(vecs.device)) if on_dev else None
+        check(lib.rfx_index_add(self.handle, ptr(vecs), vecs.shape[0], int(on_dev), ctypes.byref(first), st))
+        return first.value
+
+    def add_synthetic(self, seed: int, n: int, gen_row0: int = -1, stream=None) -> int:
+        """Append n generated rows; generator row ids start at gen_row0 (default: continue)."""
+        first = ctypes.c_int64()
+        with torch.cuda.device(self.device):
+            check(lib.rfx_index_add_synthetic(self.handle, ctypes.c_uint64(seed), int(gen_row0), int(n),
+                                              ctypes.byref(first), stream_ptr(stream)))
+        return first.value
+
+    def tombstone(self, rows) -> None:
+        import numpy as np
+        arr = np.ascontiguousarray(np.asarray(rows, dtype=np.int64))
+        with torch.cuda.device(self.device):
+            check(lib.rfx_index_tombstone(self.handle, arr.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), arr.size,
+                                          stream_ptr()))
+
+    def read(self, row0: int, n: int) -> torch.Tensor:
+        out = torch.empty((n, self.dim), dtype=self.torch_dtype, device=self._dev())
+        with torch.cuda.device(self.device):
+            check(lib.rfx_index_read(self.handle, int(row0), int(n), ptr(out), 1, stream_ptr()))
+        return out
+
+    # ---- search -------------------------------------------------------------------------------
+    def workspace_bytes(self, nq: int, k: int) -> int:
+        b = ctypes.c_size_t()
+        check(lib.rfx_search_workspace_bytes(self.handle, int(nq), int(k), ctypes.byref(b)))
+        return b.value
+
+    def _check_queries(self, q: torch.Tensor):
+        if q.dim() != 2 or q.shape[1] != self.dim or q.dtype != self.torch_dtype or not q.is_cuda:
+            raise ValueError(f"queries must be a cuda {self.torch_dtype} tensor [nq][{self.dim}]")
+        return q.contiguous()
+
+    def search(self, queries: torch.Tensor, k: int, workspace: torch.Tensor = None, stream=None):
+        """Top-k rows per query: (scores f32 [nq][k], rows int64 [nq][k]) on the device."""
+        q = self._check_queries(queries)
+        nq = q.shape[0]
+        dev = q.device
+        out_s = torch.empty((nq, k), dtype=torch.float32, device=dev)
+        out_r = torch.empty((nq, k), dtype=torch.int64, device=dev)
+        need = self.workspace_bytes(nq, k)
+        ws = workspace if workspace is not None and workspace.numel() >= need else \
+            torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+        with torch.cuda.device(dev):
+            check(lib.rfx_search(self.handle, ptr(q), nq, int(k), ptr(out_s), ptr(out_r), ptr(ws), ws.numel(),
+                                 stream_ptr(stream)))
+        return out_s, out_r
+
+    def plan(self, nq: int, k: int):
+        kern, ncand = ctypes.c_int(), ctypes.c_int64()
+        check(lib.rfx_scan_plan(self.handle, int(nq), int(k), ctypes.byref(kern), ctypes.byref(ncand)))
+        return kern.value, ncand.value
+
+    def scan(self, queries: torch.Tensor, k: int, workspace: torch.Tensor = None, stream=None):
+        """Fused scan only: per-query candidate lists (scores f32 [nq][n_cand], local rows int32)."""
+        q = self._check_queries(queries)
+        nq = q.shape[0]
+        _, ncand = self.plan(nq, k)
+        cs = torch.empty((nq, ncand), dtype=torch.float32, device=q.device)
+        cr = torch.empty((nq, ncand), dtype=torch.int32, device=q.device)
+        need = self.workspace_bytes(nq, k)
+        ws = workspace if workspace is not None and workspace.numel() >= need else \
+            torch.empty(max(need, 1), dtype=torch.uint8, device=q.device)
+        with torch.cuda.device(q.device):
+            check(lib.rfx_scan_topk(self.handle, ptr(q), nq, int(k), ptr(cs), ptr(cr), ptr(ws), ws.numel(),
+                                    stream_ptr(stream)))
+        return cs, cr
+
+
+def topk_merge(cand_s: torch.Tensor, cand_r: torch.Tensor, k: int, row_offset: int = 0, stream=None):
+    """Merge [nq][n_cand] candidates (rows int32 or int64) into the final top-k per query."""
+    if cand_s.shape != cand_r.shape or cand_s.dim() != 2:
+        raise ValueError("candidate score/row tensors must be [nq][n_cand] of equal shape")
+    if cand_r.dtype not in (torch.int32, torch.int64) or cand_s.dtype != torch.float32:
+        raise ValueError("candidates must be (float32, int32|int64)")
+    cand_s, cand_r = cand_s.contiguous(), cand_r.contiguous()
+    nq, ncand = cand_s.shape
+    out_s = torch.empty((nq, k), dtype=torch.float32, device=cand_s.device)
+    out_r = torch.empty((nq, k), dtype=torch.int64, device=cand_s.device)
+    with torch.cuda.device(cand_s.device):
+        check(lib.rfx_topk_merge(ptr(cand_s), ptr(cand_r), int(cand_r.dtype == torch.int64), nq, ncand, int(k),
+                                 int(row_offset), ptr(out_s), ptr(out_r), stream_ptr(stream)))
+    return out_s, out_r
+
+
+def synth_rows(seed: int, row0: int, n: int, dim: int, dtype: str, device: int = 0) -> torch.Tensor:
+    """Synthetic normalised rows generated on the device (same generator as the index)."""
+    out = torch.empty((n, dim), dtype=_lib.TORCH_DTYPES[dtype], device=torch.device("cuda", device))
+    with torch.cuda.device(device):
+        check(lib.rfx_synth_rows(ctypes.c_uint64(seed), int(row0), int(n), int(dim), _lib.DTYPE_CODES[dtype],
+                                 ptr(out), stream_ptr()))
+    return out

@@ -1,0 +1,53 @@
+"""Generate golden vectors FROM THE REFERENCE (run in the build container only; the reference
+does not exist on the GPU box).  Output files are committed data fixtures:
+
+  ref_normalize.json   inputs -> reference scripts/benchmark/metrics.py:_normalize outputs
+                       (the module imports only the standard library, so it is imported directly
+                       from /root/reference; nothing is stubbed)
+  sample_report.md     docs/demo/sample-report.md (BASELINE config 1 input document, data)
+  bench_questions.json scripts/benchmark/datasets/sample/questions.jsonl questions (data)
+
+Usage: python tests/golden/make_ref_golden.py [/root/reference]
+"""
+import importlib.util
+import json
+import os
+import sys
+
+REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+CASES = [
+    "", "Hello, World!", "The quick brown fox jumps over a lazy dog.", "an apple a day",
+    "RAG Foundation is a mock-mode document assistant", "UPPER lower MiXeD 123 4x5",
+    "tabs\tand\nnewlines\r\nand  double  spaces", "punct:;,.!?()[]{}<>\"'`~@#$%^&*-_=+|\\/",
+    "numbers 3.14159 and 2,718 and -42", "unicode café naïve résumé Ünïcödé",
+    "emoji 🚀 rocket and ✓ check", "İstanbul KELVIN K sign", "ＦＵＬＬＷＩＤＴＨ ａｂｃ",
+    "the the the", "a", "A An THE", "non breaking space", "snake_case and kebab-case",
+    "e-mail: someone@example.com, url https://example.com/a?b=c",
+    "What is the purpose of the /api/chat endpoint in this service?",
+    "Who wrote the song \"CompletelyMadeUpTitleXYZ\"?",
+]
+
+
+def main():
+    spec = importlib.util.spec_from_file_location("ref_metrics", os.path.join(REF, "scripts/benchmark/metrics.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    sample = open(os.path.join(REF, "docs/demo/sample-report.md"), encoding="utf-8").read()
+    qs = [json.loads(l)["question"] for l in open(os.path.join(REF, "scripts/benchmark/datasets/sample/questions.jsonl"))
+          if l.strip()]
+    cases = CASES + sample.splitlines() + [sample] + qs
+    out = [{"input": c, "normalized": mod._normalize(c)} for c in cases]
+    with open(os.path.join(HERE, "ref_normalize.json"), "w") as f:
+        json.dump({"source": "scripts/benchmark/metrics.py:13-19 (_normalize), imported from the reference",
+                   "cases": out}, f, indent=1, ensure_ascii=False)
+    with open(os.path.join(HERE, "sample_report.md"), "w", encoding="utf-8") as f:
+        f.write(sample)
+    with open(os.path.join(HERE, "bench_questions.json"), "w") as f:
+        json.dump({"source": "scripts/benchmark/datasets/sample/questions.jsonl", "questions": qs}, f, indent=1)
+    print(f"wrote {len(out)} normalize cases, sample report ({len(sample)} B), {len(qs)} questions")
+
+
+if __name__ == "__main__":
+    main()
