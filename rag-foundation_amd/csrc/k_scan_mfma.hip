@@ -258,7 +258,7 @@ MfmaPlan plan_scan_mfma(int64_t nrows, int D, int dtype, int64_t nq, int k) {
   p.bn = nq <= 64 ? 64 : (nq <= 128 ? 128 : 256);
   p.q_blocks = (int)((nq + p.bn - 1) / p.bn);
   p.nq_pad = (int64_t)p.q_blocks * p.bn;
-  const int64_t ntiles = (nrows + kBM - 1) / kBM;
+  const int64_t ntiles = std::max<int64_t>((nrows + kBM - 1) / kBM, 1);
   const int wg_per_cu = p.bn == 256 ? 1 : 2;
   int64_t blocks = std::min<int64_t>(ntiles, 256 * wg_per_cu);
   if (blocks < 1) blocks = 1;

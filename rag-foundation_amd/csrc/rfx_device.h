@@ -41,7 +41,10 @@ __host__ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
 __device__ __forceinline__ float f16_to_f32(uint16_t h) {
   return (float)__builtin_bit_cast(_Float16, h);
 }
+// The asm barrier pins the f32 value: without it LLVM folds an f64->f32->f16 chain into a single
+// f64->f16 rounding, which differs from the two-step rounding the oracle (numpy) performs.
 __device__ __forceinline__ uint16_t f32_to_f16(float f) {
+  asm volatile("" : "+v"(f));
   return __builtin_bit_cast(uint16_t, (_Float16)f);
 }
 

@@ -41,9 +41,9 @@ def gather_merge(local_s: torch.Tensor, local_r: torch.Tensor, k: int, merge, gr
     if world == 1:
         return local_s, local_r
     mine = pack(local_s, local_r)
-    out = torch.empty((world,) + tuple(mine.shape), dtype=mine.dtype, device=mine.device)
-    dist.all_gather_into_tensor(out, mine, group=group)
-    cs, cr = unpack(out)
+    out = torch.empty((world * mine.shape[0],) + tuple(mine.shape[1:]), dtype=mine.dtype, device=mine.device)
+    dist.all_gather_into_tensor(out, mine, group=group)  # ranks concatenated along dim 0
+    cs, cr = unpack(out.view((world,) + tuple(mine.shape)))
     return merge(cs, cr, k)
 
 

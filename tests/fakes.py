@@ -10,7 +10,7 @@ from oracle import synth as osynth
 from oracle import textproc
 from rfx.retriever import Hit, _chunking
 
-V, DIM = 4096, 64
+V, DIM = 4096, 768
 W_SEED, H_SEED = 0x5241475F454D4244, 0x5241475F544F4B4E
 
 

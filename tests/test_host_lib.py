@@ -1,0 +1,107 @@
+"""CPU: the C-ABI library loads, exports every symbol include/rfx.h declares, its HIP imports exist
+in the runtime torch loads, and its host-side (non-GPU) entry points match the oracle."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "rfx.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const char\*|int)\s+(rfx_\w+)\s*\(", text, re.M)))
+
+
+def test_header_declares_the_boundary():
+    syms = declared_symbols()
+    for s in ("rfx_index_create", "rfx_index_add", "rfx_index_tombstone", "rfx_index_save", "rfx_index_load",
+              "rfx_search", "rfx_scan_topk", "rfx_topk_merge", "rfx_embed", "rfx_featurize", "rfx_last_error"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    from rfx import _lib
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (rfx_\w+)", out))
+    missing = [s for s in declared_symbols() if s not in exported]
+    assert not missing, missing
+    assert set(_lib.SIGNATURES) <= exported
+
+
+def test_hip_imports_resolve_in_torch_runtime():
+    """librfx.so binds to the libamdhip64.so.7 torch already loaded: every HIP symbol it imports
+    must exist there (one HIP runtime per process)."""
+    import torch
+    from rfx import _lib
+    und = subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    hip = sorted({m.split("@")[0] for m in re.findall(r"U (\S*hip\S*)", und)})
+    rt = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    have = set(re.findall(r" T (\S+)", subprocess.run(["nm", "-D", "--defined-only", rt], capture_output=True,
+                                                      text=True, check=True).stdout))
+    have = {h.split("@")[0] for h in have}
+    assert hip and not [h for h in hip if h not in have]
+    needed = subprocess.run(["readelf", "-d", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "libamdhip64.so.7" in needed
+
+
+def test_lib_targets_gfx950_only():
+    from rfx import _lib
+    out = subprocess.run(["strings", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "gfx950" in out
+    assert "gfx942" not in out and "gfx90a" not in out
+
+
+def test_version_and_error_string():
+    from rfx import _lib
+    assert _lib.lib.rfx_version() >= 100
+    assert isinstance(_lib.lib.rfx_last_error(), bytes)
+
+
+def test_host_chunker_matches_oracle():
+    from oracle import textproc
+    from rfx import embedder
+    rng = np.random.default_rng(1)
+    for trial in range(30):
+        words = [bytes(rng.integers(33, 127, size=rng.integers(1, 9)).astype(np.uint8)) for _ in range(rng.integers(0, 300))]
+        seps = [bytes(rng.choice([b" ", b"\n", b"\t", b"  ", b"\x1c", b"\r\n"])) for _ in words]
+        raw = b"".join(w + s for w, s in zip(words, seps))
+        mt = int(rng.integers(1, 40))
+        ov = int(rng.integers(0, mt))
+        got = embedder.chunk_spans(raw, mt, ov)
+        ref = textproc.chunk_whitespace(raw, mt, ov)
+        assert got.tolist() == [list(x) for x in ref]
+
+
+def test_host_featurizer_matches_oracle(golden_dir):
+    from oracle import textproc
+    from rfx import embedder
+    raw = open(os.path.join(golden_dir, "sample_report.md"), "rb").read()
+    for mt, ov in ((3, 0), (10, 2), (200, 20)):
+        spans = textproc.chunk_whitespace(raw, mt, ov)
+        got = embedder.featurize(raw, np.array(spans), 4096, embedder.DEFAULT_HASH_SEED)
+        ref = textproc.featurize(raw, spans, 4096, embedder.DEFAULT_HASH_SEED)
+        for a, b in zip(got, ref):
+            assert np.array_equal(a, b)
+    # Unicode + clamping + articles: the product's per-chunk str.lower() path
+    texts = ["Ünïcödé CAFÉ the THE a an", "x " * 300 + "y", "", "!!", "İstanbul K"]
+    got = embedder.featurize_texts(texts, 64, 7)
+    b = [t.lower().encode() for t in texts]
+    raw = b"".join(b)
+    offs = np.cumsum([0] + [len(x) for x in b])
+    ref = textproc.featurize(raw, list(zip(offs[:-1], offs[1:])), 64, 7)
+    for a, c in zip(got, ref):
+        assert np.array_equal(a, c)
+    assert np.abs(got[2]).max() == 256  # "x" x300 clamps at 256
+
+
+def test_host_chunker_rejects_bad_config():
+    from rfx import embedder
+    with pytest.raises(ValueError):
+        embedder.chunk_spans(b"a b c", 3, 3)
+    with pytest.raises(ValueError):
+        embedder.chunk_spans(b"a b c", 0, 0)
