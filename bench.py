@@ -149,11 +149,11 @@ def main():
         "config": {"workload": f"cfg3: {a.rows}x{a.dim} {a.dtype} corpus row-sharded over {world} GPU(s), "
                                f"{a.nq} queries/batch, brute-force top-{a.k}",
                    "rows": a.rows, "dim": a.dim, "nq": a.nq, "k": a.k, "parallelism": f"rowshard{world}",
-                   "scan_kernel": "mfma" if kern == 1 else "valu"},
+                   "scan_kernel": {0: "valu", 1: "mfma128", 2: "mfma256"}[kern]},
         "achieved_hbm_gbps_per_gpu": round(achieved, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": load_pmc_traffic(workload_key),
-                     "kernel": "scan_mfma_kernel" if kern == 1 else "scan_valu_kernel",
+                     "kernel": {0: "scan_valu_kernel", 1: "scan_mfma_kernel", 2: "scan_mfma2_kernel"}[kern],
                      "kernel_ms": round(scan_ms, 4), "alg_bytes_per_launch": alg_bytes},
     }
 

@@ -81,7 +81,9 @@ __device__ __forceinline__ void list_insert(float (&ls)[KL], int (&lr)[KL], floa
   }
 }
 
-template <int DT, int BN, int KL>
+// MODE (diagnostic builds only, reached through rfx_dbg_scan_variant): 0 = full kernel,
+// 1 = no top-k epilogue (accumulators folded into one value), 2 = no MFMA (data movement only).
+template <int DT, int BN, int KL, int MODE = 0>
 __global__ __launch_bounds__(512) void scan_mfma_kernel(const uint16_t* __restrict__ X, int nrows, int D,
                                                         const uint16_t* __restrict__ Qp, int nq,
                                                         int tiles_per_block, int ntiles,
@@ -190,10 +192,29 @@ __global__ __launch_bounds__(512) void scan_mfma_kernel(const uint16_t* __restri
 #pragma unroll
       for (int m = 0; m < G::MS; ++m)
 #pragma unroll
-        for (int n = 0; n < G::NS; ++n) acc[m][n] = mfma32<DT>(a[m], b[n], acc[m][n]);
+        for (int n = 0; n < G::NS; ++n) {
+          if constexpr (MODE == 2) {
+            acc[m][n][0] += __uint_as_float(a[m].x ^ b[n].y);
+          } else {
+            acc[m][n] = mfma32<DT>(a[m], b[n], acc[m][n]);
+          }
+        }
     }
 
-    if (st % nk == nk - 1) {
+    if (MODE != 0 && st % nk == nk - 1) {
+      float t = 0.f;
+#pragma unroll
+      for (int m = 0; m < G::MS; ++m)
+#pragma unroll
+        for (int n = 0; n < G::NS; ++n) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) t += acc[m][n][r];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
+        }
+      if (t == 12345.678f) ls[0][0] = t;  // keeps the MFMA results live
+    }
+    if (MODE == 0 && st % nk == nk - 1) {
       // ---- epilogue: fold this tile's scores into the lane lists ----
       const int tile = t0 + st / nk;
       const int rbase = tile * kBM + wm * G::WROWS + 4 * half;
@@ -305,6 +326,25 @@ static int launch_mfma_bn(const MfmaPlan& p, const uint16_t* X, int nrows, int D
   if (p.bn == 64) return launch_mfma_kl<DT, 64>(p, X, nrows, D, Qp, nq, cs, cr, st);
   if (p.bn == 128) return launch_mfma_kl<DT, 128>(p, X, nrows, D, Qp, nq, cs, cr, st);
   return launch_mfma_kl<DT, 256>(p, X, nrows, D, Qp, nq, cs, cr, st);
+}
+
+int launch_scan_mfma_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, int D, const void* Qpad, int nq,
+                         float* cs, int* cr, hipStream_t st) {
+  if (!p.ok || p.bn != 256 || p.k_lane != 10) return -1;
+  const int ntiles = (nrows + kBM - 1) / kBM;
+  dim3 grid(p.blocks, p.q_blocks);
+  const uint16_t* Xh = (const uint16_t*)X;
+  const uint16_t* Qh = (const uint16_t*)Qpad;
+  if (mode == 1)
+    hipLaunchKernelGGL((scan_mfma_kernel<RFX_BF16, 256, 10, 1>), grid, dim3(512), 0, st, Xh, nrows, D, Qh, nq,
+                       p.tiles_per_block, ntiles, cs, cr, p.n_lists);
+  else if (mode == 2)
+    hipLaunchKernelGGL((scan_mfma_kernel<RFX_BF16, 256, 10, 2>), grid, dim3(512), 0, st, Xh, nrows, D, Qh, nq,
+                       p.tiles_per_block, ntiles, cs, cr, p.n_lists);
+  else
+    hipLaunchKernelGGL((scan_mfma_kernel<RFX_BF16, 256, 10, 0>), grid, dim3(512), 0, st, Xh, nrows, D, Qh, nq,
+                       p.tiles_per_block, ntiles, cs, cr, p.n_lists);
+  return 0;
 }
 
 int launch_scan_mfma(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,

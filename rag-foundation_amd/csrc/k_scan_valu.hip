@@ -269,6 +269,20 @@ int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dty
   return -1;
 }
 
+// Diagnostic streaming read (HBM ceiling calibration): every byte read once with dwordx4.
+__global__ __launch_bounds__(256) void stream_read_kernel(const uint4* __restrict__ p, int64_t n16, uint32_t* out) {
+  uint32_t acc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint4 v = p[i];
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x9e3779b9u) out[0] = acc;
+}
+
+void launch_stream_read(const void* p, int64_t bytes, uint32_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(stream_read_kernel, dim3(256 * 16), dim3(256), 0, st, (const uint4*)p, bytes / 16, out);
+}
+
 // Widen index-dtype queries to f32 (exact).
 __global__ void widen_queries_kernel(const void* __restrict__ Q, int64_t n, int dtype, float* __restrict__ out) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {

@@ -90,11 +90,11 @@ int grow(Index& ix, int64_t need, hipStream_t st) {
 
 // ---- search workspace layout ------------------------------------------------------------------
 struct SearchLayout {
-  int kernel;        // 0 = VALU, 1 = MFMA
+  int kernel;        // 0 = VALU (nq <= 8), 1 = MFMA 128×BN (nq <= 128), 2 = MFMA 256×256 (nq > 128)
   rfx::ValuPlan vp;
   rfx::MfmaPlan mp;
   int64_t n_cand;    // candidates per query
-  size_t q_off, q_bytes, cs_off, cr_off, total;
+  size_t q_off, q_bytes, tau_off, cs_off, cr_off, total;
 };
 
 size_t align_up(size_t x) { return (x + 255) / 256 * 256; }
@@ -104,13 +104,23 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
   if (nq < 0) return fail(RFX_EINVAL, "nq < 0");
   if (ix.rows >= (int64_t)INT32_MAX) return fail(RFX_EUNSUPPORTED, "shard exceeds 2^31-1 rows");
   L = SearchLayout{};
-  L.mp = rfx::plan_scan_mfma(ix.rows, ix.dim, ix.dtype, nq, k);
   L.vp = rfx::plan_scan_valu(ix.rows, ix.dim, ix.dtype, nq, k);
-  const bool use_mfma = L.mp.ok && nq > 8;
-  L.kernel = use_mfma ? 1 : 0;
-  if (use_mfma) {
+  L.kernel = 0;
+  if (nq > 8) {
+    if (nq > 128) {
+      L.mp = rfx::plan_scan_mfma2(ix.rows, ix.dim, ix.dtype, nq, k);
+      if (L.mp.ok) L.kernel = 2;
+    }
+    if (L.kernel == 0) {
+      L.mp = rfx::plan_scan_mfma(ix.rows, ix.dim, ix.dtype, nq, k);
+      if (L.mp.ok) L.kernel = 1;
+    }
+  }
+  size_t tau_bytes = 0;
+  if (L.kernel) {
     L.n_cand = L.mp.n_lists * L.mp.k_lane;
     L.q_bytes = (size_t)L.mp.nq_pad * ix.dim * 2;
+    if (L.kernel == 2) tau_bytes = (size_t)L.mp.nq_pad * 4;
   } else {
     if (!L.vp.ok) return fail(RFX_EUNSUPPORTED, "no scan kernel for dim=%d dtype=%d k=%d", ix.dim, ix.dtype, k);
     L.n_cand = (int64_t)L.vp.n_lists * L.vp.k_slot;
@@ -118,20 +128,27 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
   }
   if (ix.rows == 0) L.n_cand = 0;
   L.q_off = 0;
-  L.cs_off = align_up(L.q_bytes);
+  L.tau_off = align_up(L.q_bytes);
+  L.cs_off = L.tau_off + align_up(tau_bytes);
   L.cr_off = L.cs_off + align_up((size_t)nq * L.n_cand * 4);
   L.total = L.cr_off + align_up((size_t)nq * L.n_cand * 4);
   return RFX_OK;
 }
 
+// query staging and thresholds live in the front of ws (q_off, tau_off < cs_off)
+size_t scan_ws_bytes(const SearchLayout& L) { return L.cs_off; }
+
 int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq, float* cs, int32_t* cr,
               uint8_t* ws, hipStream_t st) {
   if (ix.rows == 0 || nq == 0) return RFX_OK;
-  if (L.kernel == 1) {
+  if (L.kernel >= 1) {
     void* qpad = ws + L.q_off;
     rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, 2, qpad, st);
-    if (rfx::launch_scan_mfma(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, cs, cr, st) != 0)
-      return fail(RFX_EUNSUPPORTED, "MFMA scan launch rejected");
+    const int rc = L.kernel == 2
+                       ? rfx::launch_scan_mfma2(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq,
+                                                (uint32_t*)(ws + L.tau_off), cs, cr, st)
+                       : rfx::launch_scan_mfma(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, cs, cr, st);
+    if (rc != 0) return fail(RFX_EUNSUPPORTED, "MFMA scan launch rejected (%d)", rc);
   } else {
     float* qf = (float*)(ws + L.q_off);
     rfx::launch_widen_queries(queries, nq * ix.dim, ix.dtype, qf, st);
@@ -436,7 +453,7 @@ int rfx_scan_topk(rfx_index_t h, const void* queries_d, int64_t nq, int k, float
   SearchLayout L;
   int rc = make_layout(*ix, nq, k, L);
   if (rc) return rc;
-  if (ws_bytes < L.q_bytes || (L.q_bytes && !ws_d)) return fail(RFX_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, L.q_bytes);
+  if (ws_bytes < scan_ws_bytes(L) || !ws_d) return fail(RFX_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, scan_ws_bytes(L));
   if (nq > 0 && !queries_d) return fail(RFX_EINVAL, "null queries");
   RFX_HIP(hipSetDevice(ix->device));
   return scan_into(*ix, L, queries_d, nq, cand_scores_d, cand_rows_d, (uint8_t*)ws_d, (hipStream_t)stream);
@@ -450,6 +467,46 @@ int rfx_topk_merge(const float* cand_scores_d, const void* cand_rows_d, int rows
   if (rfx::launch_topk_merge(cand_scores_d, cand_rows_d, rows_are_i64, nq, n_cand, k, row_offset, out_scores_d,
                              out_rows_d, (hipStream_t)stream) != 0)
     return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
+// Diagnostic entry point (not in include/rfx.h): the bf16 / nq 256 / k 10 MFMA scan with
+// parts of the kernel removed, for profiling (mode 1 = no top-k epilogue, 2 = no MFMA).
+int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k, int mode, float* cs, int32_t* cr,
+                         void* ws_d, size_t ws_bytes, void* stream) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  SearchLayout L;
+  int rc = make_layout(*ix, nq, k, L);
+  if (rc) return rc;
+  if (L.kernel == 0 || ws_bytes < scan_ws_bytes(L)) return fail(RFX_EINVAL, "variant needs an MFMA plan");
+  hipStream_t st = (hipStream_t)stream;
+  void* qpad = (uint8_t*)ws_d + L.q_off;
+  rfx::launch_pad_queries(queries_d, nq, L.mp.nq_pad, ix->dim, 2, qpad, st);
+  int rc2;
+  if (mode >= 10 && L.kernel == 2)  // 256x256 kernel ablations: mode 10 + MODE
+    rc2 = rfx::launch_scan_mfma2_dbg(L.mp, mode - 10, ix->data, (int)ix->rows, ix->dim, qpad, (int)nq,
+                                     (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st);
+  else if (mode == 3)  // the production kernel for this plan
+    rc2 = L.kernel == 2 ? rfx::launch_scan_mfma2(L.mp, ix->data, (int)ix->rows, ix->dim, ix->dtype, qpad, (int)nq,
+                                                 (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st)
+                        : rfx::launch_scan_mfma(L.mp, ix->data, (int)ix->rows, ix->dim, ix->dtype, qpad, (int)nq, cs, cr, st);
+  else
+    rc2 = rfx::launch_scan_mfma_dbg(rfx::plan_scan_mfma(ix->rows, ix->dim, ix->dtype, nq, k), mode, ix->data,
+                                    (int)ix->rows, ix->dim, qpad, (int)nq, cs, cr, st);
+  if (rc2 != 0) return fail(RFX_EUNSUPPORTED, "variant unsupported for this plan");
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
+// Diagnostic: read the whole index once with a plain dwordx4 streaming kernel (HBM ceiling).
+int rfx_dbg_stream_read(rfx_index_t h, void* scratch4_d, void* stream) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  rfx::launch_stream_read(ix->data, ix->rows * ix->row_bytes(), (uint32_t*)scratch4_d, (hipStream_t)stream);
   RFX_HIP(hipGetLastError());
   return RFX_OK;
 }

@@ -13,6 +13,7 @@ void launch_synth_rows(uint64_t seed, int64_t row0, int64_t n, int dim, int dtyp
                        hipStream_t st);
 void launch_nan_rows(void* X, const int64_t* rows_d, int64_t n, int64_t row_bytes, int dtype,
                      hipStream_t st);
+void launch_stream_read(const void* p, int64_t bytes, uint32_t* out, hipStream_t st);
 void launch_widen_queries(const void* Q, int64_t n, int dtype, float* out, hipStream_t st);
 
 // ---- VALU scan (small nq) ------------------------------------------------------------------
@@ -40,6 +41,13 @@ struct MfmaPlan {
 MfmaPlan plan_scan_mfma(int64_t nrows, int D, int dtype, int64_t nq, int k);
 int launch_scan_mfma(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad,
                      int nq, float* cs, int* cr, hipStream_t st);
+int launch_scan_mfma_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, int D, const void* Qpad, int nq,
+                         float* cs, int* cr, hipStream_t st);
+MfmaPlan plan_scan_mfma2(int64_t nrows, int D, int dtype, int64_t nq, int k);
+int launch_scan_mfma2(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st);
+int launch_scan_mfma2_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, int D, const void* Qpad, int nq,
+                          uint32_t* tau, float* cs, int* cr, hipStream_t st);
 void launch_pad_queries(const void* Q, int64_t nq, int64_t nq_pad, int D, int esz, void* out,
                         hipStream_t st);
 
