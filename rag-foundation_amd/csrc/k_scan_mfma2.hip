@@ -29,6 +29,7 @@ namespace rfx {
 typedef __attribute__((ext_vector_type(8))) __bf16 v2bf16x8;
 typedef __attribute__((ext_vector_type(8))) _Float16 v2f16x8;
 typedef __attribute__((ext_vector_type(16))) float v2f32x16;
+typedef __attribute__((ext_vector_type(4))) unsigned v2u32x4;
 
 template <int DT>
 __device__ __forceinline__ v2f32x16 mfma2(const uint4& a, const uint4& b, const v2f32x16& c) {
@@ -81,8 +82,10 @@ __device__ __forceinline__ void glds16(const void* src, uint8_t* lds_dst) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
 }
 
-// MODE (diagnostic builds only, via rfx_dbg_scan_variant): 0 full; 1 no top-k epilogue; 2 no MFMA;
-// 3 no query-row loads (B ring never refilled); 4 no corpus-row loads (A ring never refilled).
+// MODE (diagnostic builds only, via rfx_dbg_scan_variant): 0 full; 1 no top-k epilogue;
+// 2 loads + LDS reads only (no MFMA, no epilogue); 3 no query-row loads; 4 no corpus-row loads;
+// 5 MFMA + LDS reads + barriers only (the rings are filled once, then never reloaded; no epilogue);
+// 6 corpus loads only (no query reloads, no MFMA, no epilogue); 7 query loads only (ditto).
 template <int DT, int KL, int MODE = 0>
 __global__ __launch_bounds__(512) void scan_mfma2_kernel(const uint16_t* __restrict__ X, int nrows, int D,
                                                          const uint16_t* __restrict__ Qp, int nq, int tiles_per_block,
@@ -117,7 +120,7 @@ __global__ __launch_bounds__(512) void scan_mfma2_kernel(const uint16_t* __restr
     ra = ra < nrows ? ra : nrows - 1;
     rb = rb < nrows ? rb : nrows - 1;
     uint8_t* dst = lds + (st % kRingA) * kSlot;
-    if (MODE == 4) return;
+    if (MODE == 4 || ((MODE == 5 || MODE == 7) && st >= kRingA)) return;
     glds16(X + (int64_t)ra * D + koff + c0 * 8, dst + w * 1024);
     glds16(X + (int64_t)rb * D + koff + c1 * 8, dst + (w + 8) * 1024);
   };
@@ -125,7 +128,7 @@ __global__ __launch_bounds__(512) void scan_mfma2_kernel(const uint16_t* __restr
     const int tl = st / nk;
     const int koff = (st - tl * nk) * kB2K;
     uint8_t* dst = lds + kRingA * kSlot + (st % kRingB) * kSlot;
-    if (MODE == 3) return;
+    if (MODE == 3 || ((MODE == 5 || MODE == 6) && st >= kRingB)) return;
     glds16(qsrc0 + koff, dst + w * 1024);
     glds16(qsrc1 + koff, dst + (w + 8) * 1024);
   };
@@ -199,14 +202,14 @@ __global__ __launch_bounds__(512) void scan_mfma2_kernel(const uint16_t* __restr
       for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int n = 0; n < 2; ++n) {
-          if constexpr (MODE == 2)
-            acc[m][n][0] += __uint_as_float(a[m].x ^ b[n].y);
+          if constexpr (MODE == 2 || MODE == 6 || MODE == 7)
+            asm volatile("" ::"v"(__builtin_bit_cast(v2u32x4, a[m])), "v"(__builtin_bit_cast(v2u32x4, b[n])));
           else
             acc[m][n] = mfma2<DT>(a[m], b[n], acc[m][n]);
         }
     }
 
-    if (MODE == 1 && st % nk == nk - 1) {
+    if ((MODE == 1 || MODE == 2 || MODE >= 5) && st % nk == nk - 1) {
       float t = 0.f;
 #pragma unroll
       for (int m = 0; m < 4; ++m)
@@ -219,7 +222,7 @@ __global__ __launch_bounds__(512) void scan_mfma2_kernel(const uint16_t* __restr
           }
       if (t == 12345.678f) L[0][0] = 1;  // keeps the MFMA results live
     }
-    if (MODE != 1 && st % nk == nk - 1) {
+    if ((MODE == 0 || MODE == 3 || MODE == 4) && st % nk == nk - 1) {
       // ---- epilogue: fold this tile's 256 rows into the lane lists ----
       if (nk < 5) {  // the tile's threshold DMA may be younger than 4 stages: drain + barrier
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -324,7 +327,7 @@ int launch_scan_mfma2_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
                        p.tiles_per_block, ntiles, tau, cs, cr, p.n_lists);                                \
     return 0;                                                                                             \
   }
-  RFX_M2(0) RFX_M2(1) RFX_M2(2) RFX_M2(3) RFX_M2(4)
+  RFX_M2(0) RFX_M2(1) RFX_M2(2) RFX_M2(3) RFX_M2(4) RFX_M2(5) RFX_M2(6) RFX_M2(7)
 #undef RFX_M2
   return -1;
 }

@@ -70,6 +70,18 @@ std::shared_ptr<Index> get(rfx_index_t h) {
   return it == g_reg.end() ? nullptr : it->second;
 }
 
+// Invariant: rows [rows, capacity) of the device buffer hold NaN, so a scan tile that runs past
+// the last row (capacity is a multiple of 128 rows) reads rows that can never be ranked.
+int fill_tail_nan(Index& ix, hipStream_t st) {
+  const int64_t n = ix.capacity - ix.rows;
+  if (n <= 0) return RFX_OK;
+  const uint32_t pattern = ix.dtype == RFX_F32 ? 0x7fc00000u : (ix.dtype == RFX_BF16 ? 0x7fc07fc0u : 0x7e007e00u);
+  RFX_HIP(hipMemsetD32Async((hipDeviceptr_t)((uint8_t*)ix.data + ix.rows * ix.row_bytes()), (int)pattern,
+                            (size_t)(n * ix.row_bytes() / 4), st));
+  RFX_HIP(hipStreamSynchronize(st));
+  return RFX_OK;
+}
+
 int grow(Index& ix, int64_t need, hipStream_t st) {
   if (need <= ix.capacity) return RFX_OK;
   int64_t cap = ix.capacity > 0 ? ix.capacity : 1024;
@@ -85,12 +97,12 @@ int grow(Index& ix, int64_t need, hipStream_t st) {
   if (ix.data) RFX_HIP(hipFree(ix.data));  // hipFree waits for in-flight work on the old buffer
   ix.data = p;
   ix.capacity = cap;
-  return RFX_OK;
+  return fill_tail_nan(ix, st);
 }
 
 // ---- search workspace layout ------------------------------------------------------------------
 struct SearchLayout {
-  int kernel;        // 0 = VALU (nq <= 8), 1 = MFMA 128×BN (nq <= 128), 2 = MFMA 256×256 (nq > 128)
+  int kernel;        // 0 VALU (nq <= 8); 1 MFMA 128×BN (nq <= 64); 2 MFMA 256×256; 3 query-stationary MFMA
   rfx::ValuPlan vp;
   rfx::MfmaPlan mp;
   int64_t n_cand;    // candidates per query
@@ -107,7 +119,11 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
   L.vp = rfx::plan_scan_valu(ix.rows, ix.dim, ix.dtype, nq, k);
   L.kernel = 0;
   if (nq > 8) {
-    if (nq > 128) {
+    if (nq > 64) {
+      L.mp = rfx::plan_scan_mfma3(ix.rows, ix.dim, ix.dtype, nq, k);
+      if (L.mp.ok) L.kernel = 3;
+    }
+    if (L.kernel == 0 && nq > 128) {
       L.mp = rfx::plan_scan_mfma2(ix.rows, ix.dim, ix.dtype, nq, k);
       if (L.mp.ok) L.kernel = 2;
     }
@@ -120,7 +136,7 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
   if (L.kernel) {
     L.n_cand = L.mp.n_lists * L.mp.k_lane;
     L.q_bytes = (size_t)L.mp.nq_pad * ix.dim * 2;
-    if (L.kernel == 2) tau_bytes = (size_t)L.mp.nq_pad * 4;
+    if (L.kernel >= 2) tau_bytes = (size_t)L.mp.nq_pad * 4;
   } else {
     if (!L.vp.ok) return fail(RFX_EUNSUPPORTED, "no scan kernel for dim=%d dtype=%d k=%d", ix.dim, ix.dtype, k);
     L.n_cand = (int64_t)L.vp.n_lists * L.vp.k_slot;
@@ -144,10 +160,11 @@ int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq,
   if (L.kernel >= 1) {
     void* qpad = ws + L.q_off;
     rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, 2, qpad, st);
-    const int rc = L.kernel == 2
-                       ? rfx::launch_scan_mfma2(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq,
-                                                (uint32_t*)(ws + L.tau_off), cs, cr, st)
-                       : rfx::launch_scan_mfma(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, cs, cr, st);
+    uint32_t* tau = (uint32_t*)(ws + L.tau_off);
+    const int rc =
+        L.kernel == 3 ? rfx::launch_scan_mfma3(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
+        : L.kernel == 2 ? rfx::launch_scan_mfma2(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
+                        : rfx::launch_scan_mfma(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, cs, cr, st);
     if (rc != 0) return fail(RFX_EUNSUPPORTED, "MFMA scan launch rejected (%d)", rc);
   } else {
     float* qf = (float*)(ws + L.q_off);
@@ -486,13 +503,12 @@ int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k
   void* qpad = (uint8_t*)ws_d + L.q_off;
   rfx::launch_pad_queries(queries_d, nq, L.mp.nq_pad, ix->dim, 2, qpad, st);
   int rc2;
-  if (mode >= 10 && L.kernel == 2)  // 256x256 kernel ablations: mode 10 + MODE
-    rc2 = rfx::launch_scan_mfma2_dbg(L.mp, mode - 10, ix->data, (int)ix->rows, ix->dim, qpad, (int)nq,
-                                     (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st);
+  if (mode >= 10 && mode < 20)  // 256x256 kernel ablations: mode 10 + MODE
+    rc2 = rfx::launch_scan_mfma2_dbg(rfx::plan_scan_mfma2(ix->rows, ix->dim, ix->dtype, nq, k), mode - 10, ix->data,
+                                     (int)ix->rows, ix->dim, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off),
+                                     cs, cr, st);
   else if (mode == 3)  // the production kernel for this plan
-    rc2 = L.kernel == 2 ? rfx::launch_scan_mfma2(L.mp, ix->data, (int)ix->rows, ix->dim, ix->dtype, qpad, (int)nq,
-                                                 (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st)
-                        : rfx::launch_scan_mfma(L.mp, ix->data, (int)ix->rows, ix->dim, ix->dtype, qpad, (int)nq, cs, cr, st);
+    return scan_into(*ix, L, queries_d, nq, cs, cr, (uint8_t*)ws_d, st);
   else
     rc2 = rfx::launch_scan_mfma_dbg(rfx::plan_scan_mfma(ix->rows, ix->dim, ix->dtype, nq, k), mode, ix->data,
                                     (int)ix->rows, ix->dim, qpad, (int)nq, cs, cr, st);

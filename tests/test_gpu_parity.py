@@ -198,7 +198,7 @@ def test_search_tombstones(rfx):
 def test_search_mfma(rfx, dtype, nq, k):
     rindex, _ = rfx
     kern, _, _ = run_search_check(rindex, 30000, 768, dtype, nq, k)
-    assert kern == (2 if nq > 128 else 1)
+    assert kern == (3 if nq > 64 else 1)
 
 
 @pytest.mark.parametrize("n", [1, 127, 128, 129, 1000])
@@ -209,18 +209,21 @@ def test_search_mfma_ragged(rfx, n):
 
 
 @pytest.mark.parametrize("n,dim", [(1, 768), (255, 768), (256, 768), (257, 768), (70_000, 768), (5000, 64),
-                                   (5000, 128), (5000, 192), (3000, 1024)])
-def test_search_mfma2_shapes(rfx, n, dim):
-    """256x256 kernel: ragged row counts, one tile per block, and D with fewer than 5 K-stages."""
+                                   (5000, 128), (5000, 192), (3000, 1024), (1000, 1024)])
+def test_search_mfma_batched_shapes(rfx, n, dim):
+    """nq=256: query-stationary kernel (d 768/1024) or the 256x256 kernel (other d); ragged row
+    counts, one tile per block, and D with fewer than 5 K-stages."""
     rindex, _ = rfx
     kern, _, _ = run_search_check(rindex, n, dim, "bf16", 256, 10)
-    assert kern == 2
+    assert kern == (3 if dim in (768, 1024) else 2)
 
 
 @pytest.mark.parametrize("k", [1, 4, 5, 8, 16])
 def test_search_mfma2_k(rfx, k):
     rindex, _ = rfx
     kern, _, _ = run_search_check(rindex, 50_000, 768, "f16", 200, k)
+    assert kern == 3
+    kern, _, _ = run_search_check(rindex, 50_000, 640, "f16", 200, k)
     assert kern == 2
 
 
@@ -230,7 +233,15 @@ def test_search_mfma2_ties_and_tombstones(rfx):
     q64 = osynth.to_f64(osynth.synth_rows(8, 0, 1, 768, "bf16"), "bf16")
     top = int(osearch.topk(q64, rows64, 1)[1][0, 0])
     kern, s, r = run_search_check(rindex, 20000, 768, "bf16", 256, 10, dup=(top, 3), tomb=[0, 7, 19999, top + 1])
-    assert kern == 2 and r[0, 0] == 3 and r[0, 1] == top
+    assert kern == 3 and r[0, 0] == 3 and r[0, 1] == top
+
+
+@pytest.mark.parametrize("nq", [65, 128, 129, 384, 512])
+def test_search_qstationary_query_groups(rfx, nq):
+    """1..4 query groups of 128 resident queries (grid.y), padded last group."""
+    rindex, _ = rfx
+    kern, _, _ = run_search_check(rindex, 40_000, 768, "bf16", nq, 10)
+    assert kern == 3
 
 
 def test_search_mfma_dim1024(rfx):
