@@ -1,238 +1,30 @@
-// k_scan_mfma3.hip — query-stationary batched scan (d = 768 / 1024, bf16 / f16).
-//
-// Path: the retrieval half of GeminiRag.ask_stream (backend/app/services/gemini_rag.py:517-551),
-// BASELINE.json config 3 (10M×768 bf16, nq=256, k=10).  Fused scan + per-query top-k; the score
-// matrix never reaches HBM.
-//
-// Why this shape (measured on MI355X): re-streaming the query block
-// through LDS every K-stage doubled the LDS-DMA traffic and capped the corpus stream at
-// ~3.3 TB/s.  Here every wave keeps its 32 queries' MFMA B-fragments for the WHOLE of K in
-// VGPRs (D/4 registers: 192 at d=768), so only corpus rows move:
-//   * workgroup = 4 waves (one per SIMD, up to 512 VGPRs each) = 128 queries ("query group");
-//     nq = 256 is served by two groups that sweep the same row range at the same time (blocks x
-//     and x + R share an XCD under round-robin dispatch, so the second read is an L2/MALL hit;
-//     placement only affects speed, never results).
-//   * tile = 128 corpus rows; per 64-wide K-stage a 16 KB slice arrives by LDS-DMA
-//     (global_load_lds_dwordx4, 4 wave-instructions per wave) into an 8-slot ring (7 stages =
-//     112 KB in flight); one counted `s_waitcnt vmcnt(24)` + raw `s_barrier` per stage.
-//   * LDS row image: 128 B = 8 slots of 16 B, chunk c of row r in slot c ^ ((r>>1)&7):
-//     conflict-free 32-row ds_read_b128 fragment reads (the permutation rides on the LDS-DMA
-//     source address).  Each wave computes 128 rows × 32 queries = 4 sub-tiles of
-//     v_mfma_f32_32x32x16_{bf16,f16} (64 accumulator VGPRs); K is fully unrolled per tile so
-//     the resident B-fragments are statically indexed.
-//   * top-k: lane l holds query (l&31) for 64 rows per tile; sorted lane list of KL 64-bit keys
-//     (orderable score << 32 | ~row) + the cross-workgroup threshold of k_scan_mfma2.hip
-//     (device atomicMax; any value read is a lower bound of the final k-th best: exact).
-// Requires the index invariant of rfx_api.hip: rows [nrows, capacity) are NaN and capacity is a
-// multiple of 128, so the ragged last tile needs no clamping or masking.
-// Algorithmic bytes per tile: 128 * D * 2.
-#include "rfx_device.h"
+// k_scan_mfma3.hip — plan + dispatch of the query-stationary batched scan (kernel: k_scan_mfma3.h,
+// instantiated per (dtype, d) in k3_*.hip).
 #include "rfx_kernels.h"
 
 namespace rfx {
-
-typedef __attribute__((ext_vector_type(8))) __bf16 v3bf16x8;
-typedef __attribute__((ext_vector_type(8))) _Float16 v3f16x8;
-typedef __attribute__((ext_vector_type(16))) float v3f32x16;
-
-template <int DT>
-__device__ __forceinline__ v3f32x16 mfma3(const uint4& a, const uint4& b, const v3f32x16& c) {
-  if constexpr (DT == RFX_BF16)
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v3bf16x8, a), __builtin_bit_cast(v3bf16x8, b),
-                                                   c, 0, 0, 0);
-  else
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(v3f16x8, a), __builtin_bit_cast(v3f16x8, b), c,
-                                                  0, 0, 0);
-}
-
-__device__ __forceinline__ uint32_t ord3(float f) {
-  const uint32_t b = __float_as_uint(f);
-  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
-}
-__device__ __forceinline__ float unord3(uint32_t o) {
-  return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
-}
-__device__ __forceinline__ float max3f(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-
-constexpr int k3M = 128;        // rows per tile
-constexpr int k3QW = 32;        // queries per wave
-constexpr int k3QG = 128;       // queries per workgroup (4 waves)
-constexpr int k3BK = 64;        // K per stage
-constexpr int k3Slot = k3M * k3BK * 2;   // 16 KB
-constexpr int k3Ring = 8;                  // 7 stages (112 KB) in flight
-constexpr int k3GPW = k3Slot / 1024 / 4;   // LDS-DMA wave-instructions per wave per stage (4)
-constexpr int k3TauOff = k3Ring * k3Slot;  // 128 KB
-constexpr int k3Lds = k3TauOff + k3QG * 4;
-
-template <int KL>
-__device__ __forceinline__ void key_insert3(uint64_t (&L)[KL], uint64_t key) {
-#pragma unroll
-  for (int i = 0; i < KL; ++i) {
-    const bool b = key > L[i];
-    const uint64_t t = L[i];
-    L[i] = b ? key : t;
-    key = b ? t : key;
-  }
-}
-
-template <int DT, int KL, int D>
-__global__ __launch_bounds__(256, 1) void scan_mfma3_kernel(const uint16_t* __restrict__ X, int nrows,
-                                                            const uint16_t* __restrict__ Qp, int nq,
-                                                            int tiles_per_block, int ntiles, uint32_t* __restrict__ tau,
-                                                            float* __restrict__ cand_s, int* __restrict__ cand_r,
-                                                            int64_t n_lists) {
-  constexpr int NKS = D / 16;      // 16-deep MFMA k-steps
-  constexpr int NST = D / k3BK;    // stages per tile
-  __shared__ __attribute__((aligned(1024))) uint8_t lds[k3Lds];
-
-  const int tid = threadIdx.x;
-  const int w = tid >> 6, lane = tid & 63;
-  const int half = lane >> 5, l32 = lane & 31;
-  const int range = blockIdx.x;
-  const int qg = blockIdx.y * k3QG;
-  const int q = qg + w * k3QW + l32;  // this lane's query
-  const int t0 = range * tiles_per_block;
-  const int t1 = min(ntiles, t0 + tiles_per_block);
-  const int S = t1 > t0 ? (t1 - t0) * NST : 0;
-
-  // ---- resident query fragments: B[k][col] of 32x32x16, lane holds k = 16 ks + 8 half + j ----
-  uint4 bq[NKS];
-  {
-    const uint16_t* qrow = Qp + (int64_t)q * D + 8 * half;
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) bq[ks] = *(const uint4*)(qrow + 16 * ks);
-  }
-
-  // ---- LDS-DMA pattern: wave-instruction i (0..15) fills slot bytes [1024 i, +1024) = rows
-  // 8i..8i+7; lane -> (row 8i + lane/8, slot lane%8) <- chunk slot ^ ((row>>1)&7); wave w issues
-  // i = w + 4u, u = 0..3.
-  int rowoff[k3GPW], choff[k3GPW];
-#pragma unroll
-  for (int u = 0; u < k3GPW; ++u) {
-    const int r = 8 * (w + 4 * u) + (lane >> 3);
-    rowoff[u] = r;
-    choff[u] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
-  }
-  auto issue = [&](int g) {
-    const int tl = g / NST;
-    const int s = g - tl * NST;
-    const int row_base = (t0 + tl) * k3M;
-    uint8_t* dst = lds + (g % k3Ring) * k3Slot;
-#pragma unroll
-    for (int u = 0; u < k3GPW; ++u) {
-      const int r = row_base + rowoff[u];  // < capacity: rows past nrows are NaN (index invariant)
-      __builtin_amdgcn_global_load_lds((const void*)(X + (int64_t)r * D + s * k3BK + choff[u]),
-                                       (__attribute__((address_space(3))) void*)(dst + (w + 4 * u) * 1024), 16, 0, 0);
-    }
-  };
-  auto issue_tau = [&]() {
-    if (w == 0 && lane < 32)
-      __builtin_amdgcn_global_load_lds((const void*)(tau + qg + lane * 4),
-                                       (__attribute__((address_space(3))) void*)(lds + k3TauOff), 16, 0, 0);
-  };
-
-  uint64_t L[KL];
-#pragma unroll
-  for (int i = 0; i < KL; ++i) L[i] = 0ull;
-  uint32_t published = 0u;
-  const int sw = (l32 >> 1) & 7;
-  const int a_base = l32 * 128;
-
-  issue_tau();
-  // the resident query loads must land before the LDS-DMA stream starts counting
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int p = 0; p < k3Ring - 1; ++p)
-    if (p < S) issue(p);
-
-  v3f32x16 acc[4];
-  for (int tile = t0; tile < t1; ++tile) {
-    const int gbase = (tile - t0) * NST;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
-#pragma unroll
-    for (int s = 0; s < NST; ++s) {
-      const int g = gbase + s;
-      // stage g landed for this wave: at most the 6 younger stages (24 ops) remain in flight
-      if (g + 6 < S)
-        asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (s == 0 && tile > t0) issue_tau();
-      if (g + k3Ring - 1 < S) issue(g + k3Ring - 1);
-      const uint8_t* sa = lds + (g % k3Ring) * k3Slot + a_base;
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int c = 2 * kk + half;
-        const int coff = (c ^ sw) << 4;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const uint4 a = *(const uint4*)(sa + m * 32 * 128 + coff);
-          acc[m] = mfma3<DT>(a, bq[4 * s + kk], acc[m]);
-        }
-      }
-    }
-
-    // ---- epilogue: fold this tile's 256 rows into the lane list ----
-    const int rbase = tile * k3M + 4 * half;
-    float mx = -__builtin_inff();
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) mx = max3f(mx, acc[m][r], acc[m][r + 1]);  // NaN-ignoring max
-    const uint32_t shared_o = *(const uint32_t*)(lds + k3TauOff + (w * k3QW + l32) * 4);
-    const uint32_t own_o = (uint32_t)(L[KL - 1] >> 32);
-    const uint32_t thr_o = own_o > shared_o ? own_o : shared_o;
-    const float thr = thr_o ? unord3(thr_o) : -__builtin_inff();
-    if (mx >= thr) {
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float s = acc[m][r];
-          if (s >= thr) {  // NaN (tombstoned rows, rows past the end) never passes
-            const int row = rbase + m * 32 + (r & 3) + 8 * (r >> 2);
-            const uint64_t key = ((uint64_t)ord3(s) << 32) | (uint32_t)(~(uint32_t)row);
-            if (key > L[KL - 1]) key_insert3<KL>(L, key);
-          }
-        }
-      const uint32_t pub = (uint32_t)(L[KL - 1] >> 32);
-      if (pub > published && pub > shared_o) {
-        __hip_atomic_fetch_max(tau + q, pub, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        published = pub;
-      }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  if (q < nq) {
-    const int64_t o = ((int64_t)q * n_lists + (int64_t)range * 2 + half) * KL;
-#pragma unroll
-    for (int i = 0; i < KL; ++i) {
-      const uint64_t key = L[i];
-      cand_s[o + i] = key ? unord3((uint32_t)(key >> 32)) : -__builtin_inff();
-      cand_r[o + i] = key ? (int)(~(uint32_t)key) : kEmptyRow;
-    }
-  }
-}
+namespace k3 {
+#define RFX_K3_DECL(NAME)                                                                                  \
+  int NAME(int kl, dim3 grid, hipStream_t st, const uint16_t* X, int nrows, const uint16_t* Qp, int nq,      \
+           int tiles_per_block, int ntiles, uint32_t* tau, float* cs, int* cr, int64_t n_lists);
+RFX_K3_DECL(launch_bf16_768)
+RFX_K3_DECL(launch_bf16_1024)
+RFX_K3_DECL(launch_f16_768)
+RFX_K3_DECL(launch_f16_1024)
+#undef RFX_K3_DECL
+constexpr int kM = 128, kQG = 128;
+}  // namespace k3
 
 MfmaPlan plan_scan_mfma3(int64_t nrows, int D, int dtype, int64_t nq, int k) {
   MfmaPlan p{};
   p.ok = (dtype == RFX_BF16 || dtype == RFX_F16) && (D == 768 || D == 1024) && nrows > 0;
-  p.k_lane = k <= 4 ? 4 : (k <= 8 ? 8 : (k <= 10 ? 10 : (k <= 16 ? 16 : -1)));
+  p.k_lane = k <= 4 ? 4 : (k <= 10 ? 10 : (k <= 16 ? 16 : -1));
   if (p.k_lane < 0) p.ok = false;
-  p.bn = k3QG;
-  p.q_blocks = (int)((nq + k3QG - 1) / k3QG);
-  p.nq_pad = (int64_t)p.q_blocks * k3QG;
+  p.bn = k3::kQG;
+  p.q_blocks = (int)((nq + k3::kQG - 1) / k3::kQG);
+  p.nq_pad = (int64_t)p.q_blocks * k3::kQG;
   if (p.q_blocks < 1 || p.q_blocks > 256) p.ok = false;
-  const int64_t ntiles = std::max<int64_t>((nrows + k3M - 1) / k3M, 1);
+  const int64_t ntiles = std::max<int64_t>((nrows + k3::kM - 1) / k3::kM, 1);
   int64_t ranges = std::max<int64_t>(256 / std::max(p.q_blocks, 1), 1);
   ranges = std::min<int64_t>(ranges, ntiles);
   p.tiles_per_block = (int)((ntiles + ranges - 1) / ranges);
@@ -245,22 +37,14 @@ MfmaPlan plan_scan_mfma3(int64_t nrows, int D, int dtype, int64_t nq, int k) {
 int launch_scan_mfma3(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
                       uint32_t* tau, float* cs, int* cr, hipStream_t st) {
   if (!p.ok) return -1;
-  const int ntiles = (nrows + k3M - 1) / k3M;
+  const int ntiles = (nrows + k3::kM - 1) / k3::kM;
   if (hipMemsetAsync(tau, 0, (size_t)p.nq_pad * sizeof(uint32_t), st) != hipSuccess) return -2;
   dim3 grid(p.blocks, p.q_blocks);
   const uint16_t* Xh = (const uint16_t*)X;
   const uint16_t* Qh = (const uint16_t*)Qpad;
-#define RFX_K3(DTV, KV, DV)                                                                               \
-  if (dtype == DTV && p.k_lane == KV && D == DV) {                                                        \
-    hipLaunchKernelGGL((scan_mfma3_kernel<DTV, KV, DV>), grid, dim3(256), 0, st, Xh, nrows, Qh, nq,        \
-                       p.tiles_per_block, ntiles, tau, cs, cr, p.n_lists);                                \
-    return 0;                                                                                             \
-  }
-  RFX_K3(RFX_BF16, 10, 768) RFX_K3(RFX_BF16, 4, 768) RFX_K3(RFX_BF16, 8, 768) RFX_K3(RFX_BF16, 16, 768)
-  RFX_K3(RFX_F16, 10, 1024) RFX_K3(RFX_F16, 4, 1024) RFX_K3(RFX_F16, 8, 1024) RFX_K3(RFX_F16, 16, 1024)
-  RFX_K3(RFX_F16, 10, 768) RFX_K3(RFX_BF16, 10, 1024)
-#undef RFX_K3
-  return -1;
+  auto f = dtype == RFX_BF16 ? (D == 768 ? k3::launch_bf16_768 : k3::launch_bf16_1024)
+                             : (D == 768 ? k3::launch_f16_768 : k3::launch_f16_1024);
+  return f(p.k_lane, grid, st, Xh, nrows, Qh, nq, p.tiles_per_block, ntiles, tau, cs, cr, p.n_lists);
 }
 
 }  // namespace rfx
