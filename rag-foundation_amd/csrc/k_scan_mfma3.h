@@ -70,6 +70,12 @@ constexpr int k3GPW = k3Slot / 1024 / 4;   // LDS-DMA wave-instructions per wave
 constexpr int k3TauOff = k3Ring * k3Slot;  // 128 KB
 constexpr int k3Lds = k3TauOff + k3QG * 4;
 
+// LDS-DMA (global_load_lds_dwordx4) issued from inline asm; M0 = wave-uniform LDS destination.
+__device__ __forceinline__ void glds_asm(const void* src, uint32_t lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_addr)
+               : "memory", "m0");
+}
+
 template <int KL>
 __device__ __forceinline__ void key_insert3(uint64_t (&L)[KL], uint64_t key) {
 #pragma unroll
@@ -111,7 +117,9 @@ __global__ __launch_bounds__(256, 1) void scan_mfma3_kernel(const uint16_t* __re
 
   // ---- LDS-DMA pattern: wave-instruction i (0..15) fills slot bytes [1024 i, +1024) = rows
   // 8i..8i+7; lane -> (row 8i + lane/8, slot lane%8) <- chunk slot ^ ((row>>1)&7); wave w issues
-  // i = w + 4u, u = 0..3.
+  // i = w + 4u, u = 0..3.  Issued through inline asm: the compiler then cannot see a VMEM op
+  // writing LDS, so it no longer drains the whole queue (s_waitcnt vmcnt(0)) before every LDS
+  // read; ordering is ours: counted vmcnt + s_barrier before a slot is read.
   int rowoff[k3GPW], choff[k3GPW];
 #pragma unroll
   for (int u = 0; u < k3GPW; ++u) {
@@ -119,22 +127,20 @@ __global__ __launch_bounds__(256, 1) void scan_mfma3_kernel(const uint16_t* __re
     rowoff[u] = r;
     choff[u] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
   }
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
   auto issue = [&](int g) {
     const int tl = g / NST;
     const int s = g - tl * NST;
-    const int row_base = (t0 + tl) * k3M;
-    uint8_t* dst = lds + (g % k3Ring) * k3Slot;
+    const int row_base = (t0 + tl) * k3M;  // rows past nrows are NaN (index invariant), < capacity
+    const uint32_t dst = lds_base + (uint32_t)((g % k3Ring) * k3Slot) + (uint32_t)(w * 1024);
 #pragma unroll
     for (int u = 0; u < k3GPW; ++u) {
-      const int r = row_base + rowoff[u];  // < capacity: rows past nrows are NaN (index invariant)
-      __builtin_amdgcn_global_load_lds((const void*)(X + (int64_t)r * D + s * k3BK + choff[u]),
-                                       (__attribute__((address_space(3))) void*)(dst + (w + 4 * u) * 1024), 16, 0, 0);
+      const uint16_t* src = X + (int64_t)(row_base + rowoff[u]) * D + s * k3BK + choff[u];
+      glds_asm(src, __builtin_amdgcn_readfirstlane(dst + u * 4096));
     }
   };
   auto issue_tau = [&]() {
-    if (w == 0 && lane < 32)
-      __builtin_amdgcn_global_load_lds((const void*)(tau + qg + lane * 4),
-                                       (__attribute__((address_space(3))) void*)(lds + k3TauOff), 16, 0, 0);
+    if (w == 0 && lane < 32) glds_asm(tau + qg + lane * 4, __builtin_amdgcn_readfirstlane(lds_base + k3TauOff));
   };
 
   uint64_t L[KL];
@@ -144,12 +150,28 @@ __global__ __launch_bounds__(256, 1) void scan_mfma3_kernel(const uint16_t* __re
   const int sw = (l32 >> 1) & 7;
   const int a_base = l32 * 128;
 
+  // fragment reads of (stage g, k-step kk): 4 row sub-tiles of 32 rows, 16 B per lane each
+  auto read_frags = [&](int g, int kk, uint4 (&f)[4]) {
+    const uint8_t* sa = lds + (g % k3Ring) * k3Slot + a_base + (((2 * kk + half) ^ sw) << 4);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) f[m] = *(const uint4*)(sa + m * 32 * 128);
+  };
+
   issue_tau();
   // the resident query loads must land before the LDS-DMA stream starts counting
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-  for (int p = 0; p < k3Ring - 1; ++p)
+  for (int p = 0; p < k3Ring; ++p)
     if (p < S) issue(p);
+  // stage 0 (and the thresholds) landed: at most stages 1..7 (28 ops) remain in flight
+  if (S >= k3Ring)
+    asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_barrier" ::: "memory");
+
+  uint4 fa[4], fb[4];
+  if (S > 0) read_frags(0, 0, fa);
 
   v3f32x16 acc[4];
   for (int tile = t0; tile < t1; ++tile) {
@@ -161,24 +183,28 @@ __global__ __launch_bounds__(256, 1) void scan_mfma3_kernel(const uint16_t* __re
 #pragma unroll
     for (int s = 0; s < NST; ++s) {
       const int g = gbase + s;
-      // stage g landed for this wave: at most the 6 younger stages (24 ops) remain in flight
-      if (g + 6 < S)
-        asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      if (s == 0 && tile > t0) issue_tau();
-      if (g + k3Ring - 1 < S) issue(g + k3Ring - 1);
-      const uint8_t* sa = lds + (g % k3Ring) * k3Slot + a_base;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
-        const int c = 2 * kk + half;
-        const int coff = (c ^ sw) << 4;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const uint4 a = *(const uint4*)(sa + m * 32 * 128 + coff);
-          acc[m] = mfma3<DT>(a, bq[4 * s + kk], acc[m]);
+        if (kk == 3) {
+          // stage g+1 landed for this wave (younger: stages g+2..g+7 = 24 ops); every wave is
+          // done reading slot g%8 (its k-step 3 fragments were issued above), so the barrier
+          // frees the slot for stage g+8.
+          if (g + 7 < S)
+            asm volatile("s_waitcnt vmcnt(24) lgkmcnt(0)" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          asm volatile("s_barrier" ::: "memory");
+          if (s == NST - 1 && tile + 1 < t1) issue_tau();  // refreshed thresholds for the next tile
+          if (g + k3Ring < S) issue(g + k3Ring);
         }
+        // prefetch the next k-step's fragments (crossing into stage g+1 at kk == 3)
+        if (kk < 3)
+          read_frags(g, kk + 1, (kk & 1) ? fa : fb);
+        else if (g + 1 < S)
+          read_frags(g + 1, 0, (kk & 1) ? fa : fb);
+        uint4 (&cur)[4] = (kk & 1) ? fb : fa;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) acc[m] = mfma3<DT>(cur[m], bq[4 * s + kk], acc[m]);
       }
     }
 
