@@ -68,7 +68,7 @@ constexpr int k3Slot = k3M * k3BK * 2;   // 16 KB
 constexpr int k3Ring = 8;                  // 7 stages (112 KB) in flight
 constexpr int k3GPW = k3Slot / 1024 / 4;   // LDS-DMA wave-instructions per wave per stage (4)
 constexpr int k3TauOff = k3Ring * k3Slot;  // 128 KB
-constexpr int k3Lds = k3TauOff + k3QG * 4;
+constexpr int k3Lds = k3TauOff + 1024;      // thresholds: 256 slots (128 used), one DMA wave-instruction
 
 // LDS-DMA (global_load_lds_dwordx4) issued from inline asm; M0 = wave-uniform LDS destination.
 __device__ __forceinline__ void glds_asm(const void* src, uint32_t lds_addr) {
@@ -128,20 +128,23 @@ __global__ __launch_bounds__(256, 1) void scan_mfma3_kernel(const uint16_t* __re
     choff[u] = ((lane & 7) ^ ((r >> 1) & 7)) * 8;
   }
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
-  auto issue = [&](int g) {
-    const int tl = g / NST;
-    const int s = g - tl * NST;
-    const int row_base = (t0 + tl) * k3M;  // rows past nrows are NaN (index invariant), < capacity
-    const uint32_t dst = lds_base + (uint32_t)((g % k3Ring) * k3Slot) + (uint32_t)(w * 1024);
+  int laneoff[k3GPW];  // element offset of this lane's 16 B inside a [128 rows][D] tile
 #pragma unroll
-    for (int u = 0; u < k3GPW; ++u) {
-      const uint16_t* src = X + (int64_t)(row_base + rowoff[u]) * D + s * k3BK + choff[u];
-      glds_asm(src, __builtin_amdgcn_readfirstlane(dst + u * 4096));
-    }
+  for (int u = 0; u < k3GPW; ++u) laneoff[u] = rowoff[u] * D + choff[u];
+  // Stage gi -> LDS slot `slot`.  gi is clamped to the last stage so the tail of the stream issues
+  // harmless duplicate loads into already-consumed slots: every stage issues exactly k3GPW
+  // LDS-DMA ops per wave, the counted waits stay exact, and the tile body has no branches.
+  auto issue = [&](int gi, int slot) {
+    gi = gi < S ? gi : S - 1;
+    const int ti = gi / NST;
+    const int si = gi - ti * NST;
+    const uint16_t* tbase = X + (int64_t)(t0 + ti) * k3M * D + si * k3BK;
+    const uint32_t dst = lds_base + (uint32_t)(slot * k3Slot) + (uint32_t)(w * 1024);
+#pragma unroll
+    for (int u = 0; u < k3GPW; ++u) glds_asm(tbase + laneoff[u], __builtin_amdgcn_readfirstlane(dst + u * 4096));
   };
-  auto issue_tau = [&]() {
-    if (w == 0 && lane < 32) glds_asm(tau + qg + lane * 4, __builtin_amdgcn_readfirstlane(lds_base + k3TauOff));
-  };
+  // shared thresholds of this query group -> LDS (every wave, 64 lanes x 16 B = 1 KB; identical data)
+  auto issue_tau = [&]() { glds_asm(tau + qg + lane * 4, __builtin_amdgcn_readfirstlane(lds_base + k3TauOff)); };
 
   uint64_t L[KL];
 #pragma unroll
@@ -150,61 +153,60 @@ __global__ __launch_bounds__(256, 1) void scan_mfma3_kernel(const uint16_t* __re
   const int sw = (l32 >> 1) & 7;
   const int a_base = l32 * 128;
 
-  // fragment reads of (stage g, k-step kk): 4 row sub-tiles of 32 rows, 16 B per lane each
-  auto read_frags = [&](int g, int kk, uint4 (&f)[4]) {
-    const uint8_t* sa = lds + (g % k3Ring) * k3Slot + a_base + (((2 * kk + half) ^ sw) << 4);
+  // fragment reads of k-step kk from LDS slot `slot`: 4 row sub-tiles of 32 rows, 16 B per lane
+  auto read_frags = [&](int slot, int kk, uint4 (&f)[4]) {
+    const uint8_t* sa = lds + slot * k3Slot + a_base + (((2 * kk + half) ^ sw) << 4);
 #pragma unroll
     for (int m = 0; m < 4; ++m) f[m] = *(const uint4*)(sa + m * 32 * 128);
   };
 
+  if (S == 0) return;  // (cannot happen with the host plan; whole workgroup exits together)
   issue_tau();
   // the resident query loads must land before the LDS-DMA stream starts counting
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-  for (int p = 0; p < k3Ring; ++p)
-    if (p < S) issue(p);
-  // stage 0 (and the thresholds) landed: at most stages 1..7 (28 ops) remain in flight
-  if (S >= k3Ring)
-    asm volatile("s_waitcnt vmcnt(28)" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int p = 0; p < k3Ring; ++p) issue(p, p);
+  asm volatile("s_waitcnt vmcnt(28)" ::: "memory");  // stage 0 landed (stages 1..7 in flight)
   asm volatile("s_barrier" ::: "memory");
 
   uint4 fa[4], fb[4];
-  if (S > 0) read_frags(0, 0, fa);
+  read_frags(0, 0, fa);
 
   v3f32x16 acc[4];
   for (int tile = t0; tile < t1; ++tile) {
     const int gbase = (tile - t0) * NST;
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[m][r] = 0.f;
-#pragma unroll
     for (int s = 0; s < NST; ++s) {
       const int g = gbase + s;
+      const int slot = g % k3Ring;
 #pragma unroll
       for (int kk = 0; kk < 4; ++kk) {
         if (kk == 3) {
-          // stage g+1 landed for this wave (younger: stages g+2..g+7 = 24 ops); every wave is
-          // done reading slot g%8 (its k-step 3 fragments were issued above), so the barrier
-          // frees the slot for stage g+8.
-          if (g + 7 < S)
-            asm volatile("s_waitcnt vmcnt(24) lgkmcnt(0)" ::: "memory");
-          else
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+          // stage g+1 landed for this wave (younger: stages g+2..g+7 = 24 ops); all waves are
+          // done reading slot g%8 (its k-step 3 fragments were read above) -> stage g+8 may land
+          asm volatile("s_waitcnt vmcnt(24) lgkmcnt(0)" ::: "memory");
           asm volatile("s_barrier" ::: "memory");
-          if (s == NST - 1 && tile + 1 < t1) issue_tau();  // refreshed thresholds for the next tile
-          if (g + k3Ring < S) issue(g + k3Ring);
+          if (s == NST - 1) issue_tau();  // refreshed thresholds for the next tile's epilogue
+          issue(g + k3Ring, slot);
         }
         // prefetch the next k-step's fragments (crossing into stage g+1 at kk == 3)
         if (kk < 3)
-          read_frags(g, kk + 1, (kk & 1) ? fa : fb);
-        else if (g + 1 < S)
-          read_frags(g + 1, 0, (kk & 1) ? fa : fb);
+          read_frags(slot, kk + 1, (kk & 1) ? fa : fb);
+        else
+          read_frags((g + 1) % k3Ring, 0, (kk & 1) ? fa : fb);
         uint4 (&cur)[4] = (kk & 1) ? fb : fa;
+#ifndef RFX_K3_NO_SGB
+        // pin the interleave: this k-step's 4 prefetch reads go out ahead of its 4 MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+#endif
 #pragma unroll
-        for (int m = 0; m < 4; ++m) acc[m] = mfma3<DT>(cur[m], bq[4 * s + kk], acc[m]);
+        for (int m = 0; m < 4; ++m) {
+          if (s == 0 && kk == 0)
+            acc[m] = mfma3<DT>(cur[m], bq[4 * s + kk], v3f32x16{});
+          else
+            acc[m] = mfma3<DT>(cur[m], bq[4 * s + kk], acc[m]);
+        }
       }
     }
 

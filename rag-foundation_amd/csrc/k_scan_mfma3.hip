@@ -38,7 +38,7 @@ int launch_scan_mfma3(const MfmaPlan& p, const void* X, int nrows, int D, int dt
                       uint32_t* tau, float* cs, int* cr, hipStream_t st) {
   if (!p.ok) return -1;
   const int ntiles = (nrows + k3::kM - 1) / k3::kM;
-  if (hipMemsetAsync(tau, 0, (size_t)p.nq_pad * sizeof(uint32_t), st) != hipSuccess) return -2;
+  if (hipMemsetAsync(tau, 0, (size_t)(p.nq_pad + 256) * sizeof(uint32_t), st) != hipSuccess) return -2;
   dim3 grid(p.blocks, p.q_blocks);
   const uint16_t* Xh = (const uint16_t*)X;
   const uint16_t* Qh = (const uint16_t*)Qpad;
