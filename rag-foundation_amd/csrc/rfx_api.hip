@@ -119,7 +119,11 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
   L.vp = rfx::plan_scan_valu(ix.rows, ix.dim, ix.dtype, nq, k);
   L.kernel = 0;
   if (nq > 8) {
-    if (nq > 64) {
+    if (nq > 128) {
+      L.mp = rfx::plan_scan_mfma4(ix.rows, ix.dim, ix.dtype, nq, k);
+      if (L.mp.ok) L.kernel = 4;
+    }
+    if (L.kernel == 0 && nq > 64) {
       L.mp = rfx::plan_scan_mfma3(ix.rows, ix.dim, ix.dtype, nq, k);
       if (L.mp.ok) L.kernel = 3;
     }
@@ -162,7 +166,8 @@ int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq,
     rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, 2, qpad, st);
     uint32_t* tau = (uint32_t*)(ws + L.tau_off);
     const int rc =
-        L.kernel == 3 ? rfx::launch_scan_mfma3(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
+        L.kernel == 4 ? rfx::launch_scan_mfma4(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
+        : L.kernel == 3 ? rfx::launch_scan_mfma3(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
         : L.kernel == 2 ? rfx::launch_scan_mfma2(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
                         : rfx::launch_scan_mfma(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, cs, cr, st);
     if (rc != 0) return fail(RFX_EUNSUPPORTED, "MFMA scan launch rejected (%d)", rc);
@@ -503,7 +508,10 @@ int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k
   void* qpad = (uint8_t*)ws_d + L.q_off;
   rfx::launch_pad_queries(queries_d, nq, L.mp.nq_pad, ix->dim, 2, qpad, st);
   int rc2;
-  if (mode >= 10 && mode < 20)  // 256x256 kernel ablations: mode 10 + MODE
+  if (mode >= 20 && mode < 30)  // all-query-stationary kernel ablations: mode 20 + MODE
+    rc2 = rfx::launch_scan_mfma4_dbg(rfx::plan_scan_mfma4(ix->rows, ix->dim, ix->dtype, nq, k), mode - 20, ix->data,
+                                     (int)ix->rows, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st);
+  else if (mode >= 10 && mode < 20)  // 256x256 kernel ablations: mode 10 + MODE
     rc2 = rfx::launch_scan_mfma2_dbg(rfx::plan_scan_mfma2(ix->rows, ix->dim, ix->dtype, nq, k), mode - 10, ix->data,
                                      (int)ix->rows, ix->dim, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off),
                                      cs, cr, st);

@@ -192,13 +192,25 @@ def test_search_tombstones(rfx):
 
 
 # ---- search: MFMA path (batched bf16/f16) ----------------------------------------------------------
+def expected_mfma_kernel(nq, k, dim):
+    """Mirror of make_layout (rfx_api.hip): 4 = 256-query-stationary (d 768, k <= 10, nq > 128),
+    3 = 128-query-stationary (d 768/1024, k <= 16, nq > 64), 2 = 256x256 tiles, 1 = 64-query tiles."""
+    if nq > 128 and dim == 768 and k <= 10:
+        return 4
+    if nq > 64 and dim in (768, 1024) and k <= 16:
+        return 3
+    if nq > 128:
+        return 2
+    return 1
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "f16"])
 @pytest.mark.parametrize("nq", [9, 64, 100, 256, 300])
 @pytest.mark.parametrize("k", [1, 10, 16])
 def test_search_mfma(rfx, dtype, nq, k):
     rindex, _ = rfx
     kern, _, _ = run_search_check(rindex, 30000, 768, dtype, nq, k)
-    assert kern == (3 if nq > 64 else 1)
+    assert kern == expected_mfma_kernel(nq, k, 768)
 
 
 @pytest.mark.parametrize("n", [1, 127, 128, 129, 1000])
@@ -215,14 +227,14 @@ def test_search_mfma_batched_shapes(rfx, n, dim):
     counts, one tile per block, and D with fewer than 5 K-stages."""
     rindex, _ = rfx
     kern, _, _ = run_search_check(rindex, n, dim, "bf16", 256, 10)
-    assert kern == (3 if dim in (768, 1024) else 2)
+    assert kern == expected_mfma_kernel(256, 10, dim)
 
 
 @pytest.mark.parametrize("k", [1, 4, 5, 8, 16])
 def test_search_mfma2_k(rfx, k):
     rindex, _ = rfx
     kern, _, _ = run_search_check(rindex, 50_000, 768, "f16", 200, k)
-    assert kern == 3
+    assert kern == expected_mfma_kernel(200, k, 768)
     kern, _, _ = run_search_check(rindex, 50_000, 640, "f16", 200, k)
     assert kern == 2
 
@@ -233,7 +245,7 @@ def test_search_mfma2_ties_and_tombstones(rfx):
     q64 = osynth.to_f64(osynth.synth_rows(8, 0, 1, 768, "bf16"), "bf16")
     top = int(osearch.topk(q64, rows64, 1)[1][0, 0])
     kern, s, r = run_search_check(rindex, 20000, 768, "bf16", 256, 10, dup=(top, 3), tomb=[0, 7, 19999, top + 1])
-    assert kern == 3 and r[0, 0] == 3 and r[0, 1] == top
+    assert kern == 4 and r[0, 0] == 3 and r[0, 1] == top
 
 
 @pytest.mark.parametrize("nq", [65, 128, 129, 384, 512])
@@ -241,7 +253,47 @@ def test_search_qstationary_query_groups(rfx, nq):
     """1..4 query groups of 128 resident queries (grid.y), padded last group."""
     rindex, _ = rfx
     kern, _, _ = run_search_check(rindex, 40_000, 768, "bf16", nq, 10)
-    assert kern == 3
+    assert kern == expected_mfma_kernel(nq, 10, 768)
+
+
+@pytest.mark.parametrize("n", [1, 31, 32, 33, 4095, 4097, 100_003])
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_search_mfma4_ragged_rows(rfx, n, dtype):
+    """256-query-stationary kernel: 32-row tiles, ragged tails (NaN padding), fewer tiles than CUs."""
+    rindex, _ = rfx
+    kern, _, _ = run_search_check(rindex, n, 768, dtype, 256, 10)
+    assert kern == 4
+
+
+@pytest.mark.parametrize("nq,k", [(129, 10), (255, 1), (256, 4), (257, 10), (512, 5), (600, 10)])
+def test_search_mfma4_query_groups(rfx, nq, k):
+    """1..3 query groups of 256 (grid.y), padded last group, lane lists of 4 and 10."""
+    rindex, _ = rfx
+    kern, _, _ = run_search_check(rindex, 60_000, 768, "bf16", nq, k)
+    assert kern == 4
+
+
+def test_search_mfma4_many_duplicates(rfx):
+    """Twelve copies of the best row for query 0 (more than k): the lowest row ids win, in order."""
+    rindex, _ = rfx
+    n = 50_000
+    rows64 = osynth.to_f64(osynth.synth_rows(7, 0, n, 768, "bf16"), "bf16")
+    q64 = osynth.to_f64(osynth.synth_rows(8, 0, 1, 768, "bf16"), "bf16")
+    top = int(osearch.topk(q64, rows64, 1)[1][0, 0])
+    ix = rindex.DeviceIndex(768, "bf16")
+    ix.add_synthetic(7, n)
+    allr = ix.read(0, n)
+    dst = [5, 40, 41, 999, 1000, 1001, 20_000, 33_333, 40_001, 45_000, 49_998, 49_999]
+    for d in dst:
+        allr[d] = allr[top]
+    ix2 = rindex.DeviceIndex(768, "bf16")
+    ix2.add(allr)
+    q = rindex.synth_rows(8, 0, 256, 768, "bf16")
+    s, r = ix2.search(q, 10)
+    assert ix2.plan(256, 10)[0] == 4
+    want = sorted(dst + [top])[:10]
+    assert r[0].cpu().tolist() == want
+    assert float(s[0, 0]) == float(s[0, 9])
 
 
 def test_search_mfma_dim1024(rfx):

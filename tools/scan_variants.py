@@ -1,10 +1,16 @@
-"""Diagnostic: time the MFMA scan and its ablations (no epilogue / no MFMA) on the cfg3 corpus.
-Interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24).  Dev tool, not product."""
+"""Diagnostic: time the production scan and its ablations on the cfg3 corpus.
+Interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24).  Dev tool, not product.
+
+Modes: 3 = production plan; 10+M = 256x256 kernel ablation M; 20+M = 256-query-stationary kernel
+(k_scan_mfma4.h) with MODE bit flags M (1 no epilogue, 2 no MFMA, 4 contiguous ranges, 8 no corpus
+stream); 9 = plain
+dwordx4 streaming read of the corpus (HBM ceiling)."""
 import argparse
 import ctypes
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "rag-foundation_amd"))
@@ -18,6 +24,7 @@ ap.add_argument("--rows", type=int, default=10_000_000)
 ap.add_argument("--nq", type=int, default=256)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--modes", default="3,0,1,2")
+ap.add_argument("--warm-seconds", type=float, default=2.0)
 a = ap.parse_args()
 f = _lib.lib.rfx_dbg_scan_variant
 f.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -34,20 +41,30 @@ g = _lib.lib.rfx_dbg_stream_read
 g.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
 scratch = torch.zeros(4, dtype=torch.int32, device="cuda")
 modes = [int(m) for m in a.modes.split(",")] + [9]
+
+
+def launch(m):
+    if m == 9:
+        _lib.check(g(ix.handle, _lib.ptr(scratch), st))
+    else:
+        _lib.check(f(ix.handle, _lib.ptr(q), a.nq, 10, m, _lib.ptr(cs), _lib.ptr(cr), _lib.ptr(ws), ws.numel(), st))
+
+
+t_end = time.time() + a.warm_seconds  # steady-state clock before timing (MI355X_MICROARCH.md DVFS item 6)
+while time.time() < t_end:
+    launch(3)
+    torch.cuda.synchronize()
 res = {m: [] for m in modes}
 for rnd in range(a.rounds + 1):
     for m in modes:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        if m == 9:
-            _lib.check(g(ix.handle, _lib.ptr(scratch), st))
-        else:
-            _lib.check(f(ix.handle, _lib.ptr(q), a.nq, 10, m, _lib.ptr(cs), _lib.ptr(cr), _lib.ptr(ws), ws.numel(), st))
+        launch(m)
         e1.record()
         torch.cuda.synchronize()
         if rnd:
             res[m].append(e0.elapsed_time(e1))
 alg = a.rows * 768 * 2
-out = {m: {"ms_median": sorted(v)[len(v) // 2], "ms_min": min(v), "GBps": round(alg / (min(v) * 1e-3) / 1e9, 1)}
-       for m, v in res.items()}
+out = {m: {"ms_median": round(sorted(v)[len(v) // 2], 4), "ms_min": round(min(v), 4),
+           "GBps": round(alg / (min(v) * 1e-3) / 1e9, 1)} for m, v in res.items()}
 print(json.dumps(out))
