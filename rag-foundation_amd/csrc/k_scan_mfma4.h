@@ -6,24 +6,32 @@
 //
 // Why (measured, profiles/r01_v3_*): the 128-query kernel (k_scan_mfma3.h) needs two workgroups
 // per row range at nq=256.  The second read of each tile was meant to hit L2, but rocprofv3
-// FETCH_SIZE showed 24.3 GB of fabric reads per launch against 15.36 GB of corpus (1.58×), at
-// 4.9 TB/s: the stream itself was the ceiling.  Here one workgroup covers all 256 queries, so every
-// corpus byte crosses the fabric once, and each LDS fragment read feeds two MFMAs instead of one:
+// FETCH_SIZE showed 24.3 GB of fabric reads per launch against 15.36 GB of corpus (1.58×).  Here one
+// workgroup covers all 256 queries, so every corpus byte crosses the fabric once, and each LDS
+// fragment read feeds two MFMAs instead of one:
 //   * workgroup = 4 waves (one per SIMD, 512 registers each) × 64 queries.  Each wave keeps its
 //     64 queries' B-fragments for the whole of K resident: 2 × D/16 × 16 B per lane
 //     (384 registers at d = 768, split by the compiler between VGPRs and AGPRs).
-//   * tile = 32 corpus rows; a stage = 32 rows × 256 dims (16 KB) arrives by LDS-DMA
-//     (global_load_lds_dwordx4, 4 wave-instructions per wave) into a 7-slot ring, 6 stages
-//     (96 KB) in flight; one counted `s_waitcnt vmcnt(20)` + `s_barrier` per stage.
-//   * LDS row image: 512 B per row; 16-B chunk c of row r sits at position c ^ (r & 15), so the
-//     32-row ds_read_b128 fragment reads are bank-conflict free in all four lane groups (the
-//     permutation rides on the LDS-DMA source address).
+//   * tile = 32 corpus rows; a stage = 32 rows × 192 dims (12 KB) arrives by LDS-DMA
+//     (global_load_lds_dwordx4, 3 wave-instructions per wave) into a 9-slot ring, 8 stages
+//     (96 KB) in flight; one counted `s_waitcnt vmcnt` + `s_barrier` per stage.
+//   * LDS row image: 384 B per row; 16-B chunk c of row r sits at position c ^ ((r >> 1) & 7)
+//     (stays inside c's aligned 8-chunk block), so the 32-row ds_read_b128 fragment reads are
+//     bank-conflict free in all four lane groups; the permutation rides on the LDS-DMA source
+//     address.
 //   * per k-step and wave: 1 ds_read_b128 (rows × 16 k) → 2 × v_mfma_f32_32x32x16 (query blocks
 //     0 and 1), accumulators 2 × 16 registers.
 //   * top-k: lane l holds queries (l&31) and 32+(l&31) of its wave for 16 rows per tile; two
 //     sorted lane lists of KL 64-bit keys (orderable score << 32 | ~row) kept in LDS (a register
-//     holds each list's k-th best) and the cross-workgroup threshold τ (device atomicMax; any value read is a lower bound of the final k-th best, so the
-//     result stays exact whatever τ a workgroup sees).
+//     holds each list's pruning bound).
+//   * pruning threshold shared across workgroups (measured: with each list publishing its own
+//     KL-th best, 1.7 % of lane-folds still took the insert path and the epilogue cost 20 % of
+//     the kernel): per query a table of KL slots; list j (of 2 per workgroup) publishes its BEST
+//     key's score to slot j % KL by device atomicMax.  The KL slots hold scores of KL distinct
+//     rows, so min(slots) ≤ the query's KL-th best, and max(own KL-th best, min(slots)) is a valid
+//     pruning bound whatever stale value a workgroup sees: the result stays exact.  The table
+//     ([nq][12] u32) is refreshed into LDS by LDS-DMA every 4 tiles; each lane takes the min of
+//     its queries' slots every 4 tiles.
 // Requires the index invariant of rfx_api.hip: rows [nrows, capacity) are NaN and capacity is a
 // multiple of 128, so the ragged last tile needs no clamping or masking.
 // Algorithmic bytes per tile: 32 * D * esize.
@@ -61,17 +69,23 @@ __device__ __forceinline__ float max3f(float a, float b, float c) {
   return r;
 }
 
-constexpr int kTM = 32;                 // rows per tile
-constexpr int kQW = 64;                 // queries per wave
-constexpr int kQG = 256;                // queries per workgroup
-constexpr int kSK = 256;                // dims per stage
-constexpr int kSlot = kTM * kSK * 2;    // 16 KB
-constexpr int kRing = 7;                // 6 stages (96 KB) in flight
-constexpr int kGPW = kSlot / 1024 / 4;  // LDS-DMA wave-instructions per wave per stage (4)
-constexpr int kTauOff = kRing * kSlot;  // 112 KB
-constexpr int kListOff = kTauOff + 1024;  // thresholds of the 256 queries: one DMA wave-instruction
+constexpr int kTM = 32;                  // rows per tile
+constexpr int kQW = 64;                  // queries per wave
+constexpr int kQG = 256;                 // queries per workgroup
+constexpr int kSK = 192;                 // dims per stage
+constexpr int kRowB = kSK * 2;           // 384 B per row per stage
+constexpr int kSlot = kTM * kRowB;       // 12 KB
+constexpr int kRing = 9;                 // 8 stages (96 KB) in flight
+constexpr int kGPW = kSlot / 1024 / 4;   // LDS-DMA wave-instructions per wave per stage (3)
+constexpr int kTauW = 12;                // u32 per query in the threshold table (KL <= 10 slots used)
+constexpr int kTauEvery = 4;             // tiles between threshold refreshes
+constexpr int kTauOff = kRing * kSlot;   // 108 KB
+constexpr int kTauBytes = kQG * kTauW * 4;  // 12 KB: 12 DMA wave-instructions, 3 per wave
+constexpr int kListOff = kTauOff + kTauBytes;
 template <int KL>
 constexpr int lds_bytes() { return kListOff + 4 * 2 * KL * 64 * 8; }  // + lane lists [wave][2][KL][64] u64
+static_assert(lds_bytes<10>() <= 163840, "LDS budget");
+static_assert(kGPW * 4 * 1024 == kSlot && kTauBytes == 3 * 4 * 1024, "DMA pieces per wave");
 
 // LDS-DMA (global_load_lds_dwordx4) from inline asm; M0 = wave-uniform LDS destination.  The
 // compiler cannot see a VMEM op writing LDS, so it does not drain the queue before LDS reads;
@@ -80,51 +94,64 @@ __device__ __forceinline__ void glds(const void* src, uint32_t lds_addr) {
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_addr)
                : "memory", "m0");
 }
+// Same, device scope (sc1): misses this CU's L1, so other workgroups' atomicMax updates of the
+// threshold table are seen (a plain load may return an L1-resident stale line; stale stays exact).
+__device__ __forceinline__ void glds_sc1(const void* src, uint32_t lds_addr) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off sc1" ::"v"(src), "s"(lds_addr)
+               : "memory", "m0");
+}
 
+// min over the first KL threshold slots of one query (LDS image [q][kTauW] u32, 48 B per query)
 template <int KL>
-__device__ __forceinline__ void key_insert(uint64_t (&L)[KL], uint64_t key) {
-#pragma unroll
-  for (int i = 0; i < KL; ++i) {
-    const bool b = key > L[i];
-    const uint64_t t = L[i];
-    L[i] = b ? key : t;
-    key = b ? t : key;
+__device__ __forceinline__ uint32_t tau_min(const uint8_t* p) {
+  const uint4 a = *(const uint4*)p;
+  uint32_t m = min(min(a.x, a.y), min(a.z, a.w));
+  if constexpr (KL > 4) {
+    const uint4 b = *(const uint4*)(p + 16), c = *(const uint4*)(p + 32);
+    m = min(m, min(min(b.x, b.y), min(b.z, b.w)));
+    m = min(m, min(c.x, c.y));
   }
+  return m;
 }
 
 // Fold one 32×32 accumulator (16 rows of one query per lane) into the lane's list.  The list lives
-// in LDS (entry i of this lane at Ls[i * 64], best first); the lane keeps only its k-th best in a
-// register (`own`, orderable score).  Lists are read and written back only when some row of the
-// tile reaches the threshold, which after the first tiles is rare.
+// in LDS (entry i of this lane at Ls[i * 64], best first).  One register per list holds the
+// pruning bound thr_o = max(list's KL-th best, min of the shared slots) as an orderable score;
+// both terms only grow, so the bound is kept as a running max.  The list is touched only when
+// some row of the tile reaches the bound; after such an update the list's best is published to
+// its slot (device atomicMax).
 template <int KL>
-__device__ __forceinline__ void fold(const v4f32x16& acc, uint64_t* Ls, uint32_t& own, uint32_t shared_o,
-                                     int rbase, uint32_t* __restrict__ tau_q, uint32_t& published) {
+__device__ __forceinline__ void fold(const v4f32x16& acc, uint64_t* Ls, uint32_t& thr_o, int rbase,
+                                     uint32_t* __restrict__ tau, int slot_off, int& n_slow) {
   float mx = max3f(acc[0], acc[1], acc[2]);
 #pragma unroll
   for (int r = 3; r < 15; r += 2) mx = max3f(mx, acc[r], acc[r + 1]);
   mx = fmaxf(mx, acc[15]);  // NaN-ignoring max
-  const uint32_t thr_o = own > shared_o ? own : shared_o;
   const float thr = thr_o ? unord(thr_o) : -__builtin_inff();
   if (mx >= thr) {
-    uint64_t L[KL];
-#pragma unroll
-    for (int i = 0; i < KL; ++i) L[i] = Ls[i * 64];
+    ++n_slow;
+    // insert straight into the LDS list (few registers: this path runs while the resident query
+    // fragments and both accumulators occupy nearly the whole register file)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const float s = acc[r];
       if (s >= thr) {  // NaN (tombstoned rows, rows past the end) never passes
         const int row = rbase + (r & 3) + 8 * (r >> 2);
         const uint64_t key = ((uint64_t)ord(s) << 32) | (uint32_t)(~(uint32_t)row);
-        if (key > L[KL - 1]) key_insert<KL>(L, key);
+        if (key > Ls[(KL - 1) * 64]) {
+          int i = KL - 1;
+          for (; i > 0; --i) {
+            const uint64_t prev = Ls[(i - 1) * 64];
+            if (prev >= key) break;
+            Ls[i * 64] = prev;
+          }
+          Ls[i * 64] = key;
+        }
       }
     }
-#pragma unroll
-    for (int i = 0; i < KL; ++i) Ls[i * 64] = L[i];
-    own = (uint32_t)(L[KL - 1] >> 32);
-    if (own > published && own > shared_o) {
-      __hip_atomic_fetch_max(tau_q, own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      published = own;
-    }
+    const uint32_t own = (uint32_t)(Ls[(KL - 1) * 64] >> 32);
+    thr_o = own > thr_o ? own : thr_o;
+    __hip_atomic_fetch_max(tau + slot_off, (uint32_t)(Ls[0] >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -132,7 +159,9 @@ __device__ __forceinline__ void fold(const v4f32x16& acc, uint64_t* Ls, uint32_t
 // streams one contiguous window of the store (even spread over HBM channels).
 // MODE (profiling ablations, production = 0), bit flags: 1 = no top-k epilogue, 2 = no MFMA,
 // 4 = contiguous row range per block (tiles b·T .. b·T + T - 1, T = tiles_per_block),
-// 8 = no corpus stream after the prologue (MFMA + LDS reads on the first 7 stages, recycled).
+// 8 = no corpus stream after the prologue (MFMA + LDS reads on the first 9 stages, recycled),
+// 16 = count the lanes' top-k slow-path entries into cand_r[0] instead of writing candidates,
+// 32 = threshold refresh through L1 (plain load instead of sc1).
 template <int DT, int KL, int D, int MODE = 0>
 __global__ __launch_bounds__(256, 1) void scan_mfma4_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Qp,
                                                             int nq, int tiles_per_block, int ntiles,
@@ -140,8 +169,9 @@ __global__ __launch_bounds__(256, 1) void scan_mfma4_kernel(const uint16_t* __re
                                                             int* __restrict__ cand_r, int64_t n_lists) {
   constexpr int NKS = D / 16;    // 16-deep MFMA k-steps
   constexpr int NST = D / kSK;   // stages per tile
-  constexpr int KPS = kSK / 16;  // k-steps per stage (16)
-  static_assert(D % kSK == 0, "D must be a multiple of 256");
+  constexpr int KPS = kSK / 16;  // k-steps per stage (12)
+  static_assert(D % kSK == 0, "D must be a multiple of 192");
+  static_assert(KL <= 10, "threshold table holds 10 slots");
   __shared__ __attribute__((aligned(1024))) uint8_t lds[lds_bytes<KL>()];
 
   const int tid = threadIdx.x;
@@ -158,6 +188,20 @@ __global__ __launch_bounds__(256, 1) void scan_mfma4_kernel(const uint16_t* __re
                          : (range < ntiles ? (ntiles - range + nblk - 1) / nblk : 0);
   const int S = nt * NST;
   if (S == 0) return;  // (cannot happen with the host plan; whole workgroup exits together)
+  const int lst = range * 2 + half;  // this lane's list id (per query)
+
+  // ---- LDS init: threshold image and lane lists start at 0 (= "no bound" / empty) ----
+  {
+    uint4* tz = (uint4*)(lds + kTauOff);
+#pragma unroll
+    for (int i = 0; i < kTauBytes / 16 / 256; ++i) tz[tid + 256 * i] = uint4{0u, 0u, 0u, 0u};
+  }
+  uint64_t* const Ls0 = (uint64_t*)(lds + kListOff) + (w * 2 * KL) * 64 + lane;
+  uint64_t* const Ls1 = Ls0 + KL * 64;
+#pragma unroll
+  for (int i = 0; i < KL; ++i) Ls0[i * 64] = Ls1[i * 64] = 0ull;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // no LDS-DMA in flight yet: a plain barrier
 
   // ---- resident query fragments: B[k][col] of 32x32x16, lane holds k = 16 ks + 8 half + j ----
   uint4 bq0[NKS], bq1[NKS];
@@ -171,14 +215,15 @@ __global__ __launch_bounds__(256, 1) void scan_mfma4_kernel(const uint16_t* __re
     }
   }
 
-  // ---- LDS-DMA pattern: wave-instruction i (0..15) fills slot bytes [1024 i, +1024) = rows 2i, 2i+1;
-  // lane -> (row 2i + lane/32, position lane%32) <- chunk position ^ (row & 15); wave w issues
-  // i = w + 4u, u = 0..3.
+  // ---- LDS-DMA pattern: wave-instruction i (0..11) fills slot bytes [1024 i, +1024): lane L
+  // writes linear chunk n = 64 i + L = (row n / 24, position n % 24) <- source chunk
+  // position ^ ((row >> 1) & 7); wave w issues i = w + 4u, u = 0..2.
   int laneoff[kGPW];  // element offset of this lane's 16 B inside a [32 rows][D] tile (stage 0)
 #pragma unroll
   for (int u = 0; u < kGPW; ++u) {
-    const int r = 2 * (w + 4 * u) + half;
-    laneoff[u] = r * D + ((l32 ^ (r & 15)) * 8);
+    const int n = 64 * (w + 4 * u) + lane;
+    const int r = n / 24, p = n - 24 * (n / 24);
+    laneoff[u] = r * D + ((p ^ ((r >> 1) & 7)) * 8);
   }
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
   // Stage gi -> LDS slot `slot`.  gi is clamped to the last stage so the tail of the stream issues
@@ -193,26 +238,36 @@ __global__ __launch_bounds__(256, 1) void scan_mfma4_kernel(const uint16_t* __re
 #pragma unroll
     for (int u = 0; u < kGPW; ++u) glds(tbase + laneoff[u], __builtin_amdgcn_readfirstlane(dst + u * 4096));
   };
-  // shared thresholds of the 256 queries -> LDS (every wave, 64 lanes × 16 B = 1 KB; identical data)
-  auto issue_tau = [&]() { glds(tau + qg + lane * 4, __builtin_amdgcn_readfirstlane(lds_base + kTauOff)); };
-
-  uint64_t* const Ls0 = (uint64_t*)(lds + kListOff) + (w * 2 * KL) * 64 + lane;
-  uint64_t* const Ls1 = Ls0 + KL * 64;
+  // threshold table of the 256 queries -> LDS image (12 KB; wave w moves pieces w, w+4, w+8)
+  const uint32_t* tau_g = tau + (int64_t)qg * kTauW;
+  auto issue_tau = [&]() {
 #pragma unroll
-  for (int i = 0; i < KL; ++i) Ls0[i * 64] = Ls1[i * 64] = 0ull;
-  uint32_t own0 = 0u, own1 = 0u, pub0 = 0u, pub1 = 0u;
-  const uint8_t* frag_base = lds + l32 * 512;
-  const int sw = l32 & 15;
+    for (int u = 0; u < 3; ++u) {
+      const int i = w + 4 * u;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + kTauOff + i * 1024);
+      if constexpr ((MODE & 32) != 0)
+        glds(tau_g + i * 256 + lane * 4, dst);
+      else
+        glds_sc1(tau_g + i * 256 + lane * 4, dst);
+    }
+  };
+
+  uint32_t thr0 = 0u, thr1 = 0u;  // pruning bounds (orderable scores; 0 = none)
+  const int slot_off = q0 * kTauW + lst % KL;  // this lane's slot of query q0 (q0 + 32: + 32 * kTauW)
+  const uint8_t* const tq = lds + kTauOff + (w * kQW + l32) * (kTauW * 4);
+  int n_slow = 0;  // slow-path entries of this lane (diagnostic MODE 16 only; dead code otherwise)
+  const uint8_t* frag_base = lds + l32 * kRowB;
+  const int sw = (l32 >> 1) & 7;
   auto read_frag = [&](int slot, int kk) -> uint4 {
     return *(const uint4*)(frag_base + slot * kSlot + (((2 * kk + half) ^ sw) << 4));
   };
 
-  issue_tau();
   // the resident query loads must land before the LDS-DMA stream starts counting
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  issue_tau();
 #pragma unroll
   for (int p = 0; p < kRing; ++p) issue(p, p);
-  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // stage 0 landed (stages 1..6 in flight)
+  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // stage 0 landed (stages 1..8 in flight)
   asm volatile("s_barrier" ::: "memory");
 
   uint4 fa = read_frag(0, 0), fb;
@@ -220,6 +275,14 @@ __global__ __launch_bounds__(256, 1) void scan_mfma4_kernel(const uint16_t* __re
   for (int it = 0; it < nt; ++it) {
     const int tile = t0 + it * tstep;
     const int gbase = it * NST;
+    if constexpr ((MODE & 1) == 0) {
+      // refreshed threshold image (issued 2 tiles ago; any image value is a valid bound).  Here,
+      // before the tile's first MFMA, the accumulators are dead: no register pressure.
+      if ((it & (kTauEvery - 1)) == 1) {
+        thr0 = max(thr0, tau_min<KL>(tq));
+        thr1 = max(thr1, tau_min<KL>(tq + 32 * kTauW * 4));
+      }
+    }
 #pragma unroll
     for (int s = 0; s < NST; ++s) {
       const int g = gbase + s;
@@ -227,12 +290,22 @@ __global__ __launch_bounds__(256, 1) void scan_mfma4_kernel(const uint16_t* __re
 #pragma unroll
       for (int kk = 0; kk < KPS; ++kk) {
         if (kk == KPS - 1) {
-          // stage g+1 landed for this wave (younger: stages g+2..g+6 = 20 ops); every wave has read
-          // its last fragment of slot g (lgkmcnt(0) + barrier) -> stage g+7 may overwrite it
-          asm volatile("s_waitcnt vmcnt(20) lgkmcnt(0)" ::: "memory");
+          // Stage g+1 must have landed for this wave.  Ops younger than its pieces: stages
+          // g+2..g+8 (21) plus a threshold refresh (3) issued at the end of a stage g_r with
+          // g-7 <= g_r <= g-1; refreshes go out at the end of every kTauEvery-th tile (g_r ≡ 15
+          // mod 16).  lgkmcnt(0) + barrier: every wave has read its last fragment of slot g, so
+          // stage g+9 may overwrite it.
+          if constexpr ((MODE & 8) == 0) {
+            if (g >= kTauEvery * NST && (g & (kTauEvery * NST - 1)) <= 6)
+              asm volatile("s_waitcnt vmcnt(24) lgkmcnt(0)" ::: "memory");
+            else
+              asm volatile("s_waitcnt vmcnt(21) lgkmcnt(0)" ::: "memory");
+          } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          }
           asm volatile("s_barrier" ::: "memory");
           if constexpr ((MODE & 8) == 0) {
-            if (s == NST - 1) issue_tau();  // refreshed thresholds for the next tile's epilogue
+            if (s == NST - 1 && (it & (kTauEvery - 1)) == kTauEvery - 1) issue_tau();
             issue(g + kRing, slot);
           }
         }
@@ -261,16 +334,18 @@ __global__ __launch_bounds__(256, 1) void scan_mfma4_kernel(const uint16_t* __re
     // ---- epilogue: fold this tile's 32 rows into the two lane lists ----
     if constexpr ((MODE & 1) == 0) {
       const int rbase = tile * kTM + 4 * half;
-      const uint32_t* tl = (const uint32_t*)(lds + kTauOff) + w * kQW + l32;
-      fold<KL>(acc0, Ls0, own0, tl[0], rbase, tau + q0, pub0);
-      fold<KL>(acc1, Ls1, own1, tl[32], rbase, tau + q0 + 32, pub1);
+      fold<KL>(acc0, Ls0, thr0, rbase, tau, slot_off, n_slow);
+      fold<KL>(acc1, Ls1, thr1, rbase, tau, slot_off + 32 * kTauW, n_slow);
     } else {
       if (acc0[0] == 12345.f && acc1[1] == 54321.f) Ls0[0] = 1;  // keep the MFMAs live
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr ((MODE & 16) != 0) {  // diagnostic: total slow-path entries -> cand_r[0]
+    atomicAdd(cand_r, n_slow);
+    return;
+  }
 
-  const int64_t lst = (int64_t)range * 2 + half;
   if (q0 < nq) {
     const int64_t o = ((int64_t)q0 * n_lists + lst) * KL;
 #pragma unroll

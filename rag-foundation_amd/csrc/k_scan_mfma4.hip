@@ -12,6 +12,9 @@ RFX_K4_DECL(launch_f16_768)
 #undef RFX_K4_DECL
 }  // namespace k4
 
+// threshold table: [nq_pad][kTauW] u32 (k_scan_mfma4.h)
+size_t tau_bytes_mfma4(const MfmaPlan& p) { return (size_t)p.nq_pad * k4::kTauW * sizeof(uint32_t); }
+
 // 256 queries per workgroup, one workgroup per CU: grid (ranges, q_blocks) with ranges·q_blocks ≈ 256.
 MfmaPlan plan_scan_mfma4(int64_t nrows, int D, int dtype, int64_t nq, int k) {
   MfmaPlan p{};
@@ -36,7 +39,7 @@ int launch_scan_mfma4(const MfmaPlan& p, const void* X, int nrows, int D, int dt
                       uint32_t* tau, float* cs, int* cr, hipStream_t st) {
   if (!p.ok || D != 768) return -1;
   const int ntiles = (nrows + k4::kTM - 1) / k4::kTM;
-  if (hipMemsetAsync(tau, 0, (size_t)(p.nq_pad + 256) * sizeof(uint32_t), st) != hipSuccess) return -2;
+  if (hipMemsetAsync(tau, 0, tau_bytes_mfma4(p), st) != hipSuccess) return -2;
   dim3 grid(p.blocks, p.q_blocks);
   auto f = dtype == RFX_BF16 ? k4::launch_bf16_768 : k4::launch_f16_768;
   return f(p.k_lane, grid, st, (const uint16_t*)X, (const uint16_t*)Qpad, nq, p.tiles_per_block, ntiles, tau, cs, cr,
@@ -44,12 +47,13 @@ int launch_scan_mfma4(const MfmaPlan& p, const void* X, int nrows, int D, int dt
 }
 
 // Profiling ablations (bf16, d 768, KL 10), MODE bit flags of scan_mfma4_kernel:
-// 1 = no top-k epilogue, 2 = no MFMA, 4 = contiguous row range per block, 8 = no corpus stream.
+// 1 = no top-k epilogue, 2 = no MFMA, 4 = contiguous row range per block, 8 = no corpus stream,
+// 16 = count top-k slow-path entries (cand_r[0]), 32 = τ refresh through L1.
 int launch_scan_mfma4_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, const void* Qpad, int nq,
                           uint32_t* tau, float* cs, int* cr, hipStream_t st) {
   if (!p.ok || p.k_lane != 10) return -1;
   const int ntiles = (nrows + k4::kTM - 1) / k4::kTM;
-  if (hipMemsetAsync(tau, 0, (size_t)(p.nq_pad + 256) * sizeof(uint32_t), st) != hipSuccess) return -2;
+  if (hipMemsetAsync(tau, 0, tau_bytes_mfma4(p), st) != hipSuccess) return -2;
   dim3 grid(p.blocks, p.q_blocks);
   const uint16_t* Xh = (const uint16_t*)X;
   const uint16_t* Qh = (const uint16_t*)Qpad;
@@ -67,6 +71,9 @@ int launch_scan_mfma4_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
     RFX_K4_DBG(6)
     RFX_K4_DBG(8)
     RFX_K4_DBG(9)
+    RFX_K4_DBG(16)
+    RFX_K4_DBG(32)
+    RFX_K4_DBG(48)
     default:
       return -1;
   }

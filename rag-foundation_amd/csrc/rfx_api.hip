@@ -140,7 +140,10 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
   if (L.kernel) {
     L.n_cand = L.mp.n_lists * L.mp.k_lane;
     L.q_bytes = (size_t)L.mp.nq_pad * ix.dim * 2;
-    if (L.kernel >= 2) tau_bytes = (size_t)(L.mp.nq_pad + 256) * 4;  // + slack: 1 KB threshold DMA per group
+    if (L.kernel == 4)
+      tau_bytes = rfx::tau_bytes_mfma4(L.mp);
+    else if (L.kernel >= 2)
+      tau_bytes = (size_t)(L.mp.nq_pad + 256) * 4;  // + slack: 1 KB threshold DMA per group
   } else {
     if (!L.vp.ok) return fail(RFX_EUNSUPPORTED, "no scan kernel for dim=%d dtype=%d k=%d", ix.dim, ix.dtype, k);
     L.n_cand = (int64_t)L.vp.n_lists * L.vp.k_slot;
@@ -508,7 +511,7 @@ int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k
   void* qpad = (uint8_t*)ws_d + L.q_off;
   rfx::launch_pad_queries(queries_d, nq, L.mp.nq_pad, ix->dim, 2, qpad, st);
   int rc2;
-  if (mode >= 20 && mode < 30)  // all-query-stationary kernel ablations: mode 20 + MODE
+  if (mode >= 20 && mode < 100)  // all-query-stationary kernel ablations: mode 20 + MODE
     rc2 = rfx::launch_scan_mfma4_dbg(rfx::plan_scan_mfma4(ix->rows, ix->dim, ix->dtype, nq, k), mode - 20, ix->data,
                                      (int)ix->rows, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st);
   else if (mode >= 10 && mode < 20)  // 256x256 kernel ablations: mode 10 + MODE

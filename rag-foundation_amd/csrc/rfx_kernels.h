@@ -51,6 +51,7 @@ int launch_scan_mfma2_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
 MfmaPlan plan_scan_mfma3(int64_t nrows, int D, int dtype, int64_t nq, int k);
 int launch_scan_mfma3(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
                       uint32_t* tau, float* cs, int* cr, hipStream_t st);
+size_t tau_bytes_mfma4(const MfmaPlan& p);
 MfmaPlan plan_scan_mfma4(int64_t nrows, int D, int dtype, int64_t nq, int k);
 int launch_scan_mfma4(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
                       uint32_t* tau, float* cs, int* cr, hipStream_t st);

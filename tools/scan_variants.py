@@ -3,7 +3,7 @@ Interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24).  Dev 
 
 Modes: 3 = production plan; 10+M = 256x256 kernel ablation M; 20+M = 256-query-stationary kernel
 (k_scan_mfma4.h) with MODE bit flags M (1 no epilogue, 2 no MFMA, 4 contiguous ranges, 8 no corpus
-stream); 9 = plain
+stream, 16 count top-k slow-path entries, 32 τ refresh through L1); 9 = plain
 dwordx4 streaming read of the corpus (HBM ceiling)."""
 import argparse
 import ctypes
@@ -47,6 +47,8 @@ def launch(m):
     if m == 9:
         _lib.check(g(ix.handle, _lib.ptr(scratch), st))
     else:
+        if 20 <= m < 90 and (m - 20) & 16:
+            cr.zero_()
         _lib.check(f(ix.handle, _lib.ptr(q), a.nq, 10, m, _lib.ptr(cs), _lib.ptr(cr), _lib.ptr(ws), ws.numel(), st))
 
 
@@ -55,6 +57,7 @@ while time.time() < t_end:
     launch(3)
     torch.cuda.synchronize()
 res = {m: [] for m in modes}
+slow = {}
 for rnd in range(a.rounds + 1):
     for m in modes:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -64,7 +67,11 @@ for rnd in range(a.rounds + 1):
         torch.cuda.synchronize()
         if rnd:
             res[m].append(e0.elapsed_time(e1))
+        if 20 <= m < 90 and (m - 20) & 16 and rnd == a.rounds:
+            slow[m] = int(cr.flatten()[0])
 alg = a.rows * 768 * 2
 out = {m: {"ms_median": round(sorted(v)[len(v) // 2], 4), "ms_min": round(min(v), 4),
            "GBps": round(alg / (min(v) * 1e-3) / 1e9, 1)} for m, v in res.items()}
+for m, c in slow.items():
+    out[m]["slow_path_lane_entries"] = c
 print(json.dumps(out))
