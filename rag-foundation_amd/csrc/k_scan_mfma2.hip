@@ -53,11 +53,9 @@ __device__ __forceinline__ uint64_t mkkey(float s, int row) {
   return ((uint64_t)ord32(s) << 32) | (uint32_t)(~(uint32_t)row);
 }
 
-__device__ __forceinline__ float vmax3(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
+// NaN-ignoring 3-way max as plain fmaxf (hipcc emits v_max3_f32 and pads the MFMA->VALU hazard an
+// inline-asm reader of an accumulator would not get).
+__device__ __forceinline__ float vmax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 
 constexpr int kB2M = 256, kB2N = 256, kB2K = 32;
 constexpr int kRowB = kB2K * 2;                    // 64 B per operand row per stage

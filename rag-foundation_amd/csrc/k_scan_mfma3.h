@@ -54,11 +54,9 @@ __device__ __forceinline__ uint32_t ord3(float f) {
 __device__ __forceinline__ float unord3(uint32_t o) {
   return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
-__device__ __forceinline__ float max3f(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
+// NaN-ignoring 3-way max as plain fmaxf (hipcc emits v_max3_f32 and pads the MFMA->VALU hazard an
+// inline-asm reader of an accumulator would not get).
+__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 
 constexpr int k3M = 128;        // rows per tile
 constexpr int k3QW = 32;        // queries per wave

@@ -63,11 +63,10 @@ __device__ __forceinline__ uint32_t ord(float f) {
 __device__ __forceinline__ float unord(uint32_t o) {
   return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
-__device__ __forceinline__ float max3f(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
+// NaN-ignoring 3-way max.  Plain fmaxf (hipcc emits v_max3_f32): an inline-asm v_max3 reading an
+// MFMA accumulator gets no MFMA->VALU wait states from hipcc and can read it before the MFMA has
+// written it (measured: rows of a tile's first 8 accumulator registers lost, k_scan_mfma5.h).
+__device__ __forceinline__ float max3f(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
 
 constexpr int kTM = 32;                  // rows per tile
 constexpr int kQW = 64;                  // queries per wave
@@ -86,6 +85,39 @@ template <int KL>
 constexpr int lds_bytes() { return kListOff + 4 * 2 * KL * 64 * 8; }  // + lane lists [wave][2][KL][64] u64
 static_assert(lds_bytes<10>() <= 163840, "LDS budget");
 static_assert(kGPW * 4 * 1024 == kSlot && kTauBytes == 3 * 4 * 1024, "DMA pieces per wave");
+
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+
+// Buffer descriptor (4 SGPRs) for a raw byte buffer at `base` (wave-uniform).
+__device__ __forceinline__ v4i32 make_rsrc(const void* base) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  v4i32 d;
+  d.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  d.y = __builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32) & 0xffff);  // stride 0
+  d.z = -1;          // num_records: no range limit
+  d.w = 0x00020000;  // raw dword buffer (gfx9 family)
+  return d;
+}
+// LDS-DMA through a buffer descriptor: the lane address is base + 32-bit voff (one VGPR instead of
+// a 64-bit address pair).  M0 = wave-uniform LDS destination; s_nop 4 covers a descriptor freshly
+// written through v_readfirstlane (cdna_hip_programming.md §5.7 item 2).
+__device__ __forceinline__ void bdma(v4i32 rsrc, uint32_t voff, uint32_t lds_addr) {
+  asm volatile("s_nop 4\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc),
+               "s"(lds_addr)
+               : "memory", "m0");
+}
+// Same at device scope (sc1: misses this CU's L1, sees other workgroups' atomics).
+__device__ __forceinline__ void bdma_sc1(v4i32 rsrc, uint32_t voff, uint32_t lds_addr) {
+  asm volatile("s_nop 4\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen sc1 lds" ::"v"(voff),
+               "s"(rsrc), "s"(lds_addr)
+               : "memory", "m0");
+}
+// No-return device-scope unsigned max at rsrc + voff.  From asm, so hipcc neither waits for it nor
+// reloads a 64-bit address for it; it joins the wave's vmcnt queue, which only makes the kernel's
+// counted waits stricter (never looser).
+__device__ __forceinline__ void batomic_umax(v4i32 rsrc, uint32_t voff, uint32_t val) {
+  asm volatile("s_nop 4\n\tbuffer_atomic_umax %0, %1, %2, 0 offen" ::"v"(val), "v"(voff), "s"(rsrc) : "memory");
+}
 
 // LDS-DMA (global_load_lds_dwordx4) from inline asm; M0 = wave-uniform LDS destination.  The
 // compiler cannot see a VMEM op writing LDS, so it does not drain the queue before LDS reads;
@@ -121,8 +153,8 @@ __device__ __forceinline__ uint32_t tau_min(const uint8_t* p) {
 // some row of the tile reaches the bound; after such an update the list's best is published to
 // its slot (device atomicMax).
 template <int KL>
-__device__ __forceinline__ void fold(const v4f32x16& acc, uint64_t* Ls, uint32_t& thr_o, int rbase,
-                                     uint32_t* __restrict__ tau, int slot_off, int& n_slow) {
+__device__ __forceinline__ void fold(const v4f32x16& acc, uint64_t* Ls, uint32_t& thr_o, int rbase, v4i32 tau_rsrc,
+                                     uint32_t slot_voff, int& n_slow) {
   float mx = max3f(acc[0], acc[1], acc[2]);
 #pragma unroll
   for (int r = 3; r < 15; r += 2) mx = max3f(mx, acc[r], acc[r + 1]);
@@ -151,7 +183,7 @@ __device__ __forceinline__ void fold(const v4f32x16& acc, uint64_t* Ls, uint32_t
     }
     const uint32_t own = (uint32_t)(Ls[(KL - 1) * 64] >> 32);
     thr_o = own > thr_o ? own : thr_o;
-    __hip_atomic_fetch_max(tau + slot_off, (uint32_t)(Ls[0] >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    batomic_umax(tau_rsrc, slot_voff, (uint32_t)(Ls[0] >> 32));
   }
 }
 
@@ -161,7 +193,9 @@ __device__ __forceinline__ void fold(const v4f32x16& acc, uint64_t* Ls, uint32_t
 // 4 = contiguous row range per block (tiles b·T .. b·T + T - 1, T = tiles_per_block),
 // 8 = no corpus stream after the prologue (MFMA + LDS reads on the first 9 stages, recycled),
 // 16 = count the lanes' top-k slow-path entries into cand_r[0] instead of writing candidates,
-// 32 = threshold refresh through L1 (plain load instead of sc1).
+// 32 = threshold refresh through L1 (plain load instead of sc1), 64 = all of a stage's DMA pieces
+// right after the barrier (no spreading), 128 = fragment prefetch distance 1 instead of 2,
+// 256 = every corpus piece re-reads tile 0 (same LDS traffic, no HBM stream: L2 hits).
 template <int DT, int KL, int D, int MODE = 0>
 __global__ __launch_bounds__(256, 1) void scan_mfma4_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Qp,
                                                             int nq, int tiles_per_block, int ntiles,
@@ -231,12 +265,23 @@ __global__ __launch_bounds__(256, 1) void scan_mfma4_kernel(const uint16_t* __re
   // ops per wave, the counted waits stay exact, and the tile body has no branches.
   auto issue = [&](int gi, int slot) {
     gi = gi < S ? gi : S - 1;
+    if constexpr ((MODE & 256) != 0) gi = 0;
     const int ti = gi / NST;
     const int si = gi - ti * NST;
     const uint16_t* tbase = X + (int64_t)(t0 + ti * tstep) * kTM * D + si * kSK;
     const uint32_t dst = lds_base + (uint32_t)(slot * kSlot) + (uint32_t)(w * 1024);
 #pragma unroll
     for (int u = 0; u < kGPW; ++u) glds(tbase + laneoff[u], __builtin_amdgcn_readfirstlane(dst + u * 4096));
+  };
+  // one of the kGPW pieces of stage gi (same clamping)
+  auto issue_piece = [&](int gi, int slot, int u) {
+    gi = gi < S ? gi : S - 1;
+    if constexpr ((MODE & 256) != 0) gi = 0;
+    const int ti = gi / NST;
+    const int si = gi - ti * NST;
+    const uint16_t* tbase = X + (int64_t)(t0 + ti * tstep) * kTM * D + si * kSK;
+    const uint32_t dst = lds_base + (uint32_t)(slot * kSlot) + (uint32_t)(w * 1024);
+    glds(tbase + laneoff[u], __builtin_amdgcn_readfirstlane(dst + u * 4096));
   };
   // threshold table of the 256 queries -> LDS image (12 KB; wave w moves pieces w, w+4, w+8)
   const uint32_t* tau_g = tau + (int64_t)qg * kTauW;
@@ -253,7 +298,8 @@ __global__ __launch_bounds__(256, 1) void scan_mfma4_kernel(const uint16_t* __re
   };
 
   uint32_t thr0 = 0u, thr1 = 0u;  // pruning bounds (orderable scores; 0 = none)
-  const int slot_off = q0 * kTauW + lst % KL;  // this lane's slot of query q0 (q0 + 32: + 32 * kTauW)
+  const v4i32 tau_rsrc = make_rsrc(tau);
+  const uint32_t slot_voff = (uint32_t)(q0 * kTauW + lst % KL) * 4u;  // this lane's slot of query q0
   const uint8_t* const tq = lds + kTauOff + (w * kQW + l32) * (kTauW * 4);
   int n_slow = 0;  // slow-path entries of this lane (diagnostic MODE 16 only; dead code otherwise)
   const uint8_t* frag_base = lds + l32 * kRowB;
@@ -262,15 +308,33 @@ __global__ __launch_bounds__(256, 1) void scan_mfma4_kernel(const uint16_t* __re
     return *(const uint4*)(frag_base + slot * kSlot + (((2 * kk + half) ^ sw) << 4));
   };
 
+  // Schedule.  Stage h's 3 pieces per wave go out during stage h - 8, one every 4 k-steps
+  // (kSpread; bunched right after a barrier each piece costs the issuing wave ~150 cycles while
+  // its MFMAs starve), into the slot freed at stage h - 9's barrier.  Fragments are read PF
+  // k-steps ahead of their MFMAs; the stage-end wait + barrier sit at k-step KPS - PF, once every
+  // wave has issued (and, by lgkmcnt(0), received) its last read of the stage.
+  constexpr bool kSpread = (MODE & 64) == 0;
+  constexpr int PF = (MODE & 128) ? 1 : 2;
+  constexpr int NF = PF + 1;      // fragment registers in rotation
+  constexpr int KB = KPS - PF;    // k-step of the stage-end wait + barrier
+  constexpr int AHEAD = kSpread ? kRing - 1 : kRing;  // stages issued by the prologue
+  static_assert((NST * KPS) % NF == 0, "fragment rotation must realign every tile");
+
   // the resident query loads must land before the LDS-DMA stream starts counting
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   issue_tau();
 #pragma unroll
-  for (int p = 0; p < kRing; ++p) issue(p, p);
-  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // stage 0 landed (stages 1..8 in flight)
+  for (int p = 0; p < AHEAD; ++p) issue(p, p);
+  // stage 0 landed: stages 1..AHEAD-1 younger
+  if constexpr (kSpread)
+    asm volatile("s_waitcnt vmcnt(21)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
   asm volatile("s_barrier" ::: "memory");
 
-  uint4 fa = read_frag(0, 0), fb;
+  uint4 fr[NF];
+#pragma unroll
+  for (int i = 0; i < PF; ++i) fr[i] = read_frag(0, i);
   v4f32x16 acc0, acc1;
   for (int it = 0; it < nt; ++it) {
     const int tile = t0 + it * tstep;
@@ -289,12 +353,15 @@ __global__ __launch_bounds__(256, 1) void scan_mfma4_kernel(const uint16_t* __re
       const int slot = g % kRing;
 #pragma unroll
       for (int kk = 0; kk < KPS; ++kk) {
-        if (kk == KPS - 1) {
+        if constexpr (kSpread && (MODE & 8) == 0) {
+          if (kk % 4 == 0 && kk / 4 < kGPW) issue_piece(g + kRing - 1, (g + kRing - 1) % kRing, kk / 4);
+        }
+        if (kk == KB) {
           // Stage g+1 must have landed for this wave.  Ops younger than its pieces: stages
-          // g+2..g+8 (21) plus a threshold refresh (3) issued at the end of a stage g_r with
-          // g-7 <= g_r <= g-1; refreshes go out at the end of every kTauEvery-th tile (g_r ≡ 15
-          // mod 16).  lgkmcnt(0) + barrier: every wave has read its last fragment of slot g, so
-          // stage g+9 may overwrite it.
+          // g+2..g+8 (21) plus a threshold refresh (3) issued after the barrier of a stage g_r
+          // with g-7 <= g_r <= g-1; refreshes go out every kTauEvery-th tile (g_r ≡ 15 mod 16).
+          // lgkmcnt(0) + barrier: every wave has received its last fragment of slot g, so
+          // slot g may be refilled from here on.
           if constexpr ((MODE & 8) == 0) {
             if (g >= kTauEvery * NST && (g & (kTauEvery * NST - 1)) <= 6)
               asm volatile("s_waitcnt vmcnt(24) lgkmcnt(0)" ::: "memory");
@@ -306,14 +373,13 @@ __global__ __launch_bounds__(256, 1) void scan_mfma4_kernel(const uint16_t* __re
           asm volatile("s_barrier" ::: "memory");
           if constexpr ((MODE & 8) == 0) {
             if (s == NST - 1 && (it & (kTauEvery - 1)) == kTauEvery - 1) issue_tau();
-            issue(g + kRing, slot);
+            if constexpr (!kSpread) issue(g + kRing, slot);
           }
         }
-        // prefetch the next k-step's fragment (crossing into stage g+1 at the last k-step)
-        uint4& nxt = (kk & 1) ? fa : fb;
-        nxt = kk < KPS - 1 ? read_frag(slot, kk + 1) : read_frag((g + 1) % kRing, 0);
-        const uint4& cur = (kk & 1) ? fb : fa;
         const int ks = s * KPS + kk;
+        // prefetch k-step kk + PF (crossing into stage g+1 after the barrier)
+        fr[(ks + PF) % NF] = kk + PF < KPS ? read_frag(slot, kk + PF) : read_frag((g + 1) % kRing, kk + PF - KPS);
+        const uint4& cur = fr[ks % NF];
         if constexpr ((MODE & 2) == 0) {
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // the prefetch read goes out first
           __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
@@ -334,8 +400,8 @@ __global__ __launch_bounds__(256, 1) void scan_mfma4_kernel(const uint16_t* __re
     // ---- epilogue: fold this tile's 32 rows into the two lane lists ----
     if constexpr ((MODE & 1) == 0) {
       const int rbase = tile * kTM + 4 * half;
-      fold<KL>(acc0, Ls0, thr0, rbase, tau, slot_off, n_slow);
-      fold<KL>(acc1, Ls1, thr1, rbase, tau, slot_off + 32 * kTauW, n_slow);
+      fold<KL>(acc0, Ls0, thr0, rbase, tau_rsrc, slot_voff, n_slow);
+      fold<KL>(acc1, Ls1, thr1, rbase, tau_rsrc, slot_voff + 32 * kTauW * 4, n_slow);
     } else {
       if (acc0[0] == 12345.f && acc1[1] == 54321.f) Ls0[0] = 1;  // keep the MFMAs live
     }

@@ -48,10 +48,14 @@ int launch_scan_mfma4(const MfmaPlan& p, const void* X, int nrows, int D, int dt
 
 // Profiling ablations (bf16, d 768, KL 10), MODE bit flags of scan_mfma4_kernel:
 // 1 = no top-k epilogue, 2 = no MFMA, 4 = contiguous row range per block, 8 = no corpus stream,
-// 16 = count top-k slow-path entries (cand_r[0]), 32 = τ refresh through L1.
-int launch_scan_mfma4_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, const void* Qpad, int nq,
+// 16 = count top-k slow-path entries (cand_r[0]), 32 = τ refresh through L1, 64 = DMA pieces
+// bunched after the barrier, 128 = fragment prefetch distance 1,
+// 256 = corpus pieces all re-read tile 0.
+int launch_scan_mfma4_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, int dtype, const void* Qpad, int nq,
                           uint32_t* tau, float* cs, int* cr, hipStream_t st) {
-  if (!p.ok || p.k_lane != 10) return -1;
+  if (!p.ok) return -1;
+  if (mode == 0) return launch_scan_mfma4(p, X, nrows, 768, dtype, Qpad, nq, tau, cs, cr, st);  // production plan
+  if (p.k_lane != 10) return -1;
   const int ntiles = (nrows + k4::kTM - 1) / k4::kTM;
   if (hipMemsetAsync(tau, 0, tau_bytes_mfma4(p), st) != hipSuccess) return -2;
   dim3 grid(p.blocks, p.q_blocks);
@@ -74,6 +78,10 @@ int launch_scan_mfma4_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
     RFX_K4_DBG(16)
     RFX_K4_DBG(32)
     RFX_K4_DBG(48)
+    RFX_K4_DBG(64)
+    RFX_K4_DBG(128)
+    RFX_K4_DBG(192)
+    RFX_K4_DBG(257)
     default:
       return -1;
   }

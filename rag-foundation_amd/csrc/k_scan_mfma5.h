@@ -1,0 +1,311 @@
+// k_scan_mfma5.h — all-query-stationary batched scan, two waves per SIMD.
+//
+// Path: the retrieval half of GeminiRag.ask_stream (backend/app/services/gemini_rag.py:517-551),
+// BASELINE.json config 3 (10M×768 bf16, nq=256, k=10).  Fused scan + per-query top-k; the score
+// matrix never reaches HBM.
+//
+// Why (measured on MI355X with k_scan_mfma4.h's ablations, profiles/r01_*): with ONE wave per SIMD
+// (64 resident queries, 512 registers) the corpus stream (2.4 ms alone) and the MFMA work (2.6 ms
+// alone) did not overlap: 4.0 ms together.  Every LDS-DMA issue (~100-150 cycles under load), every
+// stage barrier and every top-k epilogue stalled the only MFMA issuer of its SIMD.  Here a
+// workgroup is 8 waves, two per SIMD, each with 32 resident queries (192 VGPRs of B-fragments, no
+// AGPR copies): while one wave issues DMA, waits at a barrier or folds its tile into its top-k
+// list, its SIMD partner keeps the matrix core busy.  The price is one ds_read_b128 per MFMA
+// instead of one per two (LDS at ~half its read bandwidth).
+//   * workgroup = 8 waves × 32 queries = 256 queries; every corpus byte crosses the fabric once.
+//   * tile = 32 corpus rows; a stage = 32 rows × 256 dims (16 KB) arrives by LDS-DMA
+//     (global_load_lds_dwordx4, 2 wave-instructions per wave, spread over the stage's k-steps)
+//     into a 6-slot ring, 5 stages (80 KB) in flight; one counted `s_waitcnt vmcnt` + `s_barrier`
+//     per stage.
+//   * LDS row image: 512 B per row; 16-B chunk c of row r at position c ^ (r & 15): conflict-free
+//     32-row ds_read_b128 fragment reads (the permutation rides on the DMA source address).
+//   * per k-step and wave: 1 ds_read_b128 (32 rows × 16 k) → 1 v_mfma_f32_32x32x16.
+//   * top-k and the cross-workgroup pruning bound: as k_scan_mfma4.h (lane lists in LDS, per-query
+//     10-slot best-of-list table refreshed by DMA every 4 tiles) — one list per lane.
+// Requires the index invariant of rfx_api.hip: rows [nrows, capacity) are NaN and capacity is a
+// multiple of 128, so the ragged last tile needs no clamping or masking.
+// Algorithmic bytes per tile: 32 * D * esize.
+#pragma once
+#include "k_scan_mfma4.h"
+
+namespace rfx {
+namespace k5 {
+
+using k4::batomic_umax;
+using k4::bdma;
+using k4::bdma_sc1;
+using k4::fold;
+using k4::make_rsrc;
+using k4::v4i32;
+using k4::glds;
+using k4::glds_sc1;
+using k4::mfma;
+using k4::tau_min;
+using k4::unord;
+using k4::v4f32x16;
+
+constexpr int kWaves = 8;
+constexpr int kTM = 32;                   // rows per tile
+constexpr int kQW = 32;                   // queries per wave
+constexpr int kQG = kWaves * kQW;         // 256 queries per workgroup
+constexpr int kSK = 256;                  // dims per stage
+constexpr int kRowB = kSK * 2;            // 512 B per row per stage
+constexpr int kSlot = kTM * kRowB;        // 16 KB
+constexpr int kRing = 6;                  // 5 stages (80 KB) in flight
+constexpr int kGPW = kSlot / 1024 / kWaves;  // LDS-DMA wave-instructions per wave per stage (2)
+constexpr int kTauW = 16;                 // u32 per query in the threshold table (KL <= 10 used)
+constexpr int kTauEvery = 4;              // tiles between threshold refreshes
+constexpr int kTauOff = kRing * kSlot;    // 96 KB
+constexpr int kTauBytes = kQG * kTauW * 4;  // 16 KB: 16 DMA wave-instructions, 2 per wave
+constexpr int kTauGPW = kTauBytes / 1024 / kWaves;
+constexpr int kListOff = kTauOff + kTauBytes;
+template <int KL>
+constexpr int lds_bytes() { return kListOff + kWaves * KL * 64 * 8; }  // + lane lists [wave][KL][64] u64
+static_assert(lds_bytes<10>() <= 163840, "LDS budget");
+static_assert(kGPW == 2 && kTauGPW == 2, "DMA pieces per wave");
+
+// MODE (profiling ablations, production = 0), bit flags: 1 = no top-k epilogue, 2 = no MFMA,
+// 8 = no corpus stream after the prologue, 16 = count the lanes' top-k slow-path entries into
+// cand_r[0] instead of writing candidates, 64 = a stage's DMA pieces bunched after the barrier,
+// 128 = fragment prefetch distance 1 instead of 2, 256 = every corpus piece re-reads tile 0,
+// 512 = shared threshold table ignored, 1024 = no pruning bound at all, 2048 = threshold table
+// refreshed by a plain (L1) buffer LDS-DMA, 4096 = by global_load_lds sc1, 8192 = write each lane
+// list's final pruning bound instead of candidates, 16384 = stage-end wait drains vmcnt to 0,
+// 32768 = stage-end wait one stage stricter.
+template <int DT, int KL, int D, int MODE = 0>
+__global__ __launch_bounds__(512, 1) void scan_mfma5_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Qp,
+                                                            int nq, int ntiles, uint32_t* __restrict__ tau,
+                                                            float* __restrict__ cand_s, int* __restrict__ cand_r,
+                                                            int64_t n_lists) {
+  constexpr int NKS = D / 16;    // 16-deep MFMA k-steps
+  constexpr int NST = D / kSK;   // stages per tile
+  constexpr int KPS = kSK / 16;  // k-steps per stage (16)
+  static_assert(D % kSK == 0, "D must be a multiple of 256");
+  static_assert(KL <= 10, "threshold table holds 10 slots");
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[lds_bytes<KL>()];
+
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, lane = tid & 63;
+  const int half = lane >> 5, l32 = lane & 31;
+  const int range = blockIdx.x;
+  const int qg = blockIdx.y * kQG;
+  const int q = qg + w * kQW + l32;  // this lane's query
+  // tile mapping: block b of B takes tiles b, b + B, ... (the grid streams one window of the store)
+  const int nblk = gridDim.x;
+  const int nt = range < ntiles ? (ntiles - range + nblk - 1) / nblk : 0;
+  const int S = nt * NST;
+  if (S == 0) return;  // (cannot happen with the host plan; whole workgroup exits together)
+  const int lst = range * 2 + half;  // this lane's list id (per query)
+
+  // ---- LDS init: threshold image and lane lists start at 0 (= "no bound" / empty) ----
+  {
+    uint4* tz = (uint4*)(lds + kTauOff);
+#pragma unroll
+    for (int i = 0; i < kTauBytes / 16 / 512; ++i) tz[tid + 512 * i] = uint4{0u, 0u, 0u, 0u};
+  }
+  uint64_t* const Ls = (uint64_t*)(lds + kListOff) + (w * KL) * 64 + lane;
+#pragma unroll
+  for (int i = 0; i < KL; ++i) Ls[i * 64] = 0ull;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // no LDS-DMA in flight yet: a plain barrier
+
+  // ---- resident query fragments: B[k][col] of 32x32x16, lane holds k = 16 ks + 8 half + j ----
+  uint4 bq[NKS];
+  {
+    const uint16_t* qa = Qp + (int64_t)q * D + 8 * half;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) bq[ks] = *(const uint4*)(qa + 16 * ks);
+  }
+
+  // ---- LDS-DMA pattern: wave-instruction i (0..15) fills slot bytes [1024 i, +1024) = rows 2i,
+  // 2i+1; lane -> (row 2i + lane/32, position lane%32) <- source chunk position ^ (row & 15);
+  // wave w issues i = w + 8u, u = 0..1.
+  uint32_t laneoff[kGPW];  // byte offset of this lane's 16 B inside a [32 rows][D] tile (stage 0)
+#pragma unroll
+  for (int u = 0; u < kGPW; ++u) {
+    const int r = 2 * (w + kWaves * u) + half;
+    laneoff[u] = (uint32_t)(r * D + ((l32 ^ (r & 15)) * 8)) * 2u;
+  }
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
+  // piece u of stage gi -> LDS slot `slot`.  gi is clamped to the last stage so the tail of the
+  // stream issues harmless duplicate loads into free slots: every stage issues exactly kGPW
+  // LDS-DMA ops per wave and the counted waits stay exact.
+  auto issue_piece = [&](int gi, int slot, int u) {
+    gi = gi < S ? gi : S - 1;
+    if constexpr ((MODE & 256) != 0) gi = 0;
+    const int ti = gi / NST;
+    const int si = gi - ti * NST;
+    const uint16_t* tbase = X + (int64_t)(range + ti * nblk) * kTM * D + si * kSK;
+    const uint32_t dst = lds_base + (uint32_t)(slot * kSlot) + (uint32_t)((w + kWaves * u) * 1024);
+    bdma(make_rsrc(tbase), laneoff[u], __builtin_amdgcn_readfirstlane(dst));
+  };
+  // threshold table of the 256 queries -> LDS image (16 KB; wave w moves pieces w, w + 8)
+  const v4i32 tau_rsrc = make_rsrc(tau);
+  auto issue_tau = [&]() {
+#pragma unroll
+    for (int u = 0; u < kTauGPW; ++u) {
+      const int i = w + kWaves * u;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + kTauOff + i * 1024);
+      const uint32_t off = (uint32_t)(qg * kTauW * 4 + tid * 16 + u * kWaves * 1024);
+      if constexpr ((MODE & 2048) != 0)
+        bdma(tau_rsrc, off, dst);
+      else if constexpr ((MODE & 4096) != 0)
+        glds_sc1((const uint8_t*)tau + off, dst);
+      else
+        bdma_sc1(tau_rsrc, off, dst);
+    }
+  };
+
+  uint32_t thr = 0u;  // pruning bound (orderable score; 0 = none)
+  const uint32_t slot_voff = (uint32_t)(q * kTauW + lst % KL) * 4u;
+  const uint8_t* const tq = lds + kTauOff + (w * kQW + l32) * (kTauW * 4);
+  int n_slow = 0;  // slow-path entries of this lane (diagnostic MODE 16 only; dead code otherwise)
+  const uint8_t* frag_base = lds + l32 * kRowB;
+  const int sw = l32 & 15;
+  auto read_frag = [&](int slot, int kk) -> uint4 {
+    return *(const uint4*)(frag_base + slot * kSlot + (((2 * kk + half) ^ sw) << 4));
+  };
+
+  // Schedule.  Stage h's pieces go out during stage h - 5, at k-steps 0 and 8 (spread), into the
+  // slot freed at stage h - 6's barrier.  Fragments are read PF k-steps ahead of their MFMA; the
+  // stage-end wait + barrier sit at k-step KPS - PF, once every wave has issued (and, by
+  // lgkmcnt(0), received) its last read of the stage.
+  constexpr bool kSpread = (MODE & 64) == 0;
+  constexpr int PF = (MODE & 128) ? 1 : 2;
+  constexpr int NF = PF + 1;      // fragment registers in rotation
+  constexpr int KB = KPS - PF;    // k-step of the stage-end wait + barrier
+  constexpr int AHEAD = kSpread ? kRing - 1 : kRing;  // stages issued by the prologue
+  constexpr int YNG = (kRing - 2) * kGPW;             // ops younger than the next stage (8)
+  static_assert((NST * KPS) % NF == 0, "fragment rotation must realign every tile");
+
+  // the resident query loads must land before the LDS-DMA stream starts counting
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  issue_tau();
+#pragma unroll
+  for (int p = 0; p < AHEAD; ++p)
+#pragma unroll
+    for (int u = 0; u < kGPW; ++u) issue_piece(p, p, u);
+  // stage 0 landed: stages 1..AHEAD-1 younger
+  if constexpr (kSpread)
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(YNG) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(YNG + kGPW) : "memory");
+  asm volatile("s_barrier" ::: "memory");
+
+  uint4 fr[NF];
+#pragma unroll
+  for (int i = 0; i < PF; ++i) fr[i] = read_frag(0, i);
+  v4f32x16 acc;
+  for (int it = 0; it < nt; ++it) {
+    const int tile = range + it * nblk;
+    const int gbase = it * NST;
+    if constexpr ((MODE & 1) == 0) {
+      // refreshed threshold image (issued 2 tiles ago; any image value is a valid bound), read
+      // before the tile's first MFMA while the accumulator is dead.
+      if constexpr ((MODE & 512) == 0)
+        if ((it & (kTauEvery - 1)) == 1) thr = max(thr, tau_min<KL>(tq));
+    }
+    // A threshold refresh (kTauGPW ops) issued after the barrier of stage g_r = last stage of tile
+    // it_r ≡ 3 (mod 4) is younger than stage g+1's pieces iff g-4 <= g_r <= g-1: in tile it ≡ 0
+    // at every stage and in tile it ≡ 1 at stage 0, once such a refresh exists (it_r >= 3).
+    const bool tau_young12 = it >= kTauEvery && (it & (kTauEvery - 1)) == 0;
+    const bool tau_young0 = tau_young12 || (it > kTauEvery && (it & (kTauEvery - 1)) == 1);
+#pragma unroll
+    for (int s = 0; s < NST; ++s) {
+      const int g = gbase + s;
+      const int slot = g % kRing;
+#pragma unroll
+      for (int kk = 0; kk < KPS; ++kk) {
+        if constexpr (kSpread && (MODE & 8) == 0) {
+          if (kk % 8 == 0 && kk / 8 < kGPW) issue_piece(g + kRing - 1, (g + kRing - 1) % kRing, kk / 8);
+        }
+        if (kk == KB) {
+          // stage g+1 landed for this wave: ops younger than its pieces = stages g+2..g+5 (8)
+          // [+ a threshold refresh (2)]; lgkmcnt(0) + barrier: every wave has received its last
+          // fragment of slot g, which may be refilled from here on.
+          if constexpr ((MODE & 16384) != 0) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // diagnostic: drain
+          } else if constexpr ((MODE & 32768) != 0) {
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(YNG - kGPW) : "memory");  // one stage stricter
+          } else if constexpr ((MODE & 8) == 0) {
+            if (s == 0 ? tau_young0 : tau_young12)
+              asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(YNG + kTauGPW) : "memory");
+            else
+              asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(YNG) : "memory");
+          } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          }
+          asm volatile("s_barrier" ::: "memory");
+          if constexpr ((MODE & 8) == 0) {
+            if (s == NST - 1 && (it & (kTauEvery - 1)) == kTauEvery - 1) issue_tau();
+            if constexpr (!kSpread) {
+#pragma unroll
+              for (int u = 0; u < kGPW; ++u) issue_piece(g + kRing, slot, u);
+            }
+          }
+        }
+        const int ks = s * KPS + kk;
+        // prefetch k-step kk + PF (crossing into stage g+1 after the barrier)
+        fr[(ks + PF) % NF] = kk + PF < KPS ? read_frag(slot, kk + PF) : read_frag((g + 1) % kRing, kk + PF - KPS);
+        const uint4& cur = fr[ks % NF];
+        if constexpr ((MODE & 2) == 0) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // the prefetch read goes out first
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          acc = ks == 0 ? mfma<DT>(cur, bq[ks], v4f32x16{}) : mfma<DT>(cur, bq[ks], acc);
+        } else {
+          if (ks == 0) acc = v4f32x16{};
+          acc[kk & 15] += __uint_as_float(cur.x & 0x3f000000u);  // keep the reads live
+        }
+      }
+    }
+
+    // ---- epilogue: fold this tile's 32 rows into the lane list ----
+    if constexpr ((MODE & 1) == 0) {
+      if constexpr ((MODE & 1024) != 0) {
+        uint32_t t0 = 0u;  // diagnostic: no pruning bound at all
+        fold<KL>(acc, Ls, t0, tile * kTM + 4 * half, tau_rsrc, slot_voff, n_slow);
+      } else {
+        fold<KL>(acc, Ls, thr, tile * kTM + 4 * half, tau_rsrc, slot_voff, n_slow);
+      }
+    } else {
+      if (acc[0] == 12345.f) Ls[0] = 1;  // keep the MFMAs live
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr ((MODE & 16) != 0) {  // diagnostic: total slow-path entries -> cand_r[0]
+    atomicAdd(cand_r, n_slow);
+    return;
+  }
+  if constexpr ((MODE & 8192) != 0) {  // diagnostic: final pruning bound of every lane list
+    cand_s[(int64_t)q * n_lists + lst] = thr ? unord(thr) : -__builtin_inff();
+    cand_r[(int64_t)q * n_lists + lst] = (int)(tau_min<KL>(tq) == thr);
+    return;
+  }
+  if (q < nq) {
+    const int64_t o = ((int64_t)q * n_lists + lst) * KL;
+#pragma unroll
+    for (int i = 0; i < KL; ++i) {
+      const uint64_t key = Ls[i * 64];
+      cand_s[o + i] = key ? unord((uint32_t)(key >> 32)) : -__builtin_inff();
+      cand_r[o + i] = key ? (int)(~(uint32_t)key) : kEmptyRow;
+    }
+  }
+}
+
+// one translation unit per (dtype, D) instantiates the kernel for the lane-list sizes KL in {4, 10}
+#define RFX_K5_INSTANTIATE(DTV, DV, NAME)                                                                  \
+  int NAME(int kl, dim3 grid, hipStream_t st, const uint16_t* X, const uint16_t* Qp, int nq, int ntiles,     \
+           uint32_t* tau, float* cs, int* cr, int64_t n_lists) {                                           \
+    if (kl == 4)                                                                                         \
+      hipLaunchKernelGGL((scan_mfma5_kernel<DTV, 4, DV>), grid, dim3(512), 0, st, X, Qp, nq, ntiles, tau, cs, \
+                         cr, n_lists);                                                                    \
+    else if (kl == 10)                                                                                   \
+      hipLaunchKernelGGL((scan_mfma5_kernel<DTV, 10, DV>), grid, dim3(512), 0, st, X, Qp, nq, ntiles, tau,  \
+                         cs, cr, n_lists);                                                                \
+    else                                                                                                 \
+      return -1;                                                                                         \
+    return 0;                                                                                            \
+  }
+
+}  // namespace k5
+}  // namespace rfx

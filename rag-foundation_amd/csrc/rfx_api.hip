@@ -120,8 +120,8 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
   L.kernel = 0;
   if (nq > 8) {
     if (nq > 128) {
-      L.mp = rfx::plan_scan_mfma4(ix.rows, ix.dim, ix.dtype, nq, k);
-      if (L.mp.ok) L.kernel = 4;
+      L.mp = rfx::plan_scan_mfma5(ix.rows, ix.dim, ix.dtype, nq, k);
+      if (L.mp.ok) L.kernel = 5;
     }
     if (L.kernel == 0 && nq > 64) {
       L.mp = rfx::plan_scan_mfma3(ix.rows, ix.dim, ix.dtype, nq, k);
@@ -140,7 +140,9 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
   if (L.kernel) {
     L.n_cand = L.mp.n_lists * L.mp.k_lane;
     L.q_bytes = (size_t)L.mp.nq_pad * ix.dim * 2;
-    if (L.kernel == 4)
+    if (L.kernel == 5)  // (>= the kernel-4 table: the debug path may run either on this layout)
+      tau_bytes = std::max(rfx::tau_bytes_mfma5(L.mp), rfx::tau_bytes_mfma4(L.mp));
+    else if (L.kernel == 4)
       tau_bytes = rfx::tau_bytes_mfma4(L.mp);
     else if (L.kernel >= 2)
       tau_bytes = (size_t)(L.mp.nq_pad + 256) * 4;  // + slack: 1 KB threshold DMA per group
@@ -169,7 +171,8 @@ int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq,
     rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, 2, qpad, st);
     uint32_t* tau = (uint32_t*)(ws + L.tau_off);
     const int rc =
-        L.kernel == 4 ? rfx::launch_scan_mfma4(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
+        L.kernel == 5 ? rfx::launch_scan_mfma5(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
+        : L.kernel == 4 ? rfx::launch_scan_mfma4(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
         : L.kernel == 3 ? rfx::launch_scan_mfma3(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
         : L.kernel == 2 ? rfx::launch_scan_mfma2(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
                         : rfx::launch_scan_mfma(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, cs, cr, st);
@@ -511,9 +514,12 @@ int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k
   void* qpad = (uint8_t*)ws_d + L.q_off;
   rfx::launch_pad_queries(queries_d, nq, L.mp.nq_pad, ix->dim, 2, qpad, st);
   int rc2;
-  if (mode >= 20 && mode < 100)  // all-query-stationary kernel ablations: mode 20 + MODE
+  if (mode >= 1000 && mode < 100000)  // two-waves-per-SIMD kernel ablations: mode 1000 + MODE
+    rc2 = rfx::launch_scan_mfma5_dbg(rfx::plan_scan_mfma5(ix->rows, ix->dim, ix->dtype, nq, k), mode - 1000, ix->data,
+                                     (int)ix->rows, ix->dtype, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st);
+  else if (mode >= 20 && mode < 1000)  // all-query-stationary kernel ablations: mode 20 + MODE
     rc2 = rfx::launch_scan_mfma4_dbg(rfx::plan_scan_mfma4(ix->rows, ix->dim, ix->dtype, nq, k), mode - 20, ix->data,
-                                     (int)ix->rows, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st);
+                                     (int)ix->rows, ix->dtype, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st);
   else if (mode >= 10 && mode < 20)  // 256x256 kernel ablations: mode 10 + MODE
     rc2 = rfx::launch_scan_mfma2_dbg(rfx::plan_scan_mfma2(ix->rows, ix->dim, ix->dtype, nq, k), mode - 10, ix->data,
                                      (int)ix->rows, ix->dim, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off),

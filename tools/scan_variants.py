@@ -47,7 +47,7 @@ def launch(m):
     if m == 9:
         _lib.check(g(ix.handle, _lib.ptr(scratch), st))
     else:
-        if 20 <= m < 90 and (m - 20) & 16:
+        if 20 <= m < 1000 and (m - 20) & 16:
             cr.zero_()
         _lib.check(f(ix.handle, _lib.ptr(q), a.nq, 10, m, _lib.ptr(cs), _lib.ptr(cr), _lib.ptr(ws), ws.numel(), st))
 
@@ -67,7 +67,7 @@ for rnd in range(a.rounds + 1):
         torch.cuda.synchronize()
         if rnd:
             res[m].append(e0.elapsed_time(e1))
-        if 20 <= m < 90 and (m - 20) & 16 and rnd == a.rounds:
+        if 20 <= m < 1000 and (m - 20) & 16 and rnd == a.rounds:
             slow[m] = int(cr.flatten()[0])
 alg = a.rows * 768 * 2
 out = {m: {"ms_median": round(sorted(v)[len(v) // 2], 4), "ms_min": round(min(v), 4),
