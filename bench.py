@@ -6,7 +6,8 @@ Workload (BASELINE.json configs[2], the config the metric is quoted on):
   (one process per GPU, torch.distributed backend "nccl" = RCCL) and each step ends with the
   all-gather of per-shard top-k + merge (rfx.dist) — total work fixed => "scaling": "strong".
 A step = one batch: fused MFMA scan + per-shard merge (+ all-gather + global merge for N > 1),
-inputs already resident in HBM.
+inputs already resident in HBM.  For N > 1 the shard's top-k goes out as packed records
+(rfx_topk_merge_records), one RCCL all-gather, one HIP merge of the gathered records.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--nq Q] [--k K] [--dim D]
                        [--dtype bf16|f16|f32] [--no-cpu-baseline]
@@ -77,7 +78,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from rfx import dist as rdist
-    from rfx.index import DeviceIndex, synth_rows, topk_merge
+    from rfx.index import DeviceIndex, synth_rows, topk_merge, topk_merge_records
 
     dev = torch.device("cuda", local)
     r0, r1 = rdist.shard_range(a.rows, rank, world)
@@ -86,6 +87,8 @@ def main():
     ix.add_synthetic(a.seed, n_local, gen_row0=r0)
     q = synth_rows(a.seed + 1, 0, a.nq, a.dim, a.dtype, local)
     kern, n_cand = ix.plan(a.nq, a.k)
+    list_len = ix.list_len(a.nq, a.k)
+    rec = torch.empty((a.nq, a.k, 2), dtype=torch.int64, device=dev)
     ws = torch.empty(max(ix.workspace_bytes(a.nq, a.k), 1), dtype=torch.uint8, device=dev)
     cs = torch.empty((a.nq, n_cand), dtype=torch.float32, device=dev)
     cr = torch.empty((a.nq, n_cand), dtype=torch.int32, device=dev)
@@ -101,10 +104,11 @@ def main():
                                 stream_ptr(stream)))
         if ev is not None:
             ev[1].record(stream)
-        s, r = topk_merge(cs, cr, a.k, row_offset=r0, stream=stream)
-        if world > 1:
-            s, r = rdist.gather_merge(s, r, a.k, topk_merge)
-        return s, r
+        if world == 1:
+            return topk_merge(cs, cr, a.k, row_offset=r0, stream=stream, list_len=list_len)
+        # rank-local top-k as all-gather records (global rows), one collective, one HIP merge
+        topk_merge_records(cs, cr, a.k, row_offset=r0, stream=stream, list_len=list_len, out=rec)
+        return rdist.gather_merge_records(rec, a.k, stream=stream)
 
     for _ in range(a.warmup):
         step()

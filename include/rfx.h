@@ -113,6 +113,23 @@ int rfx_scan_topk(rfx_index_t h, const void* queries_d, int64_t nq, int k, float
 int rfx_topk_merge(const float* cand_scores_d, const void* cand_rows_d, int rows_are_i64,
                    int64_t nq, int64_t n_cand, int k, int64_t row_offset, float* out_scores_d,
                    int64_t* out_rows_d, void* stream);
+/* Same, told that the candidates of a query are sorted lists of list_len entries (best first), as
+ * rfx_scan_topk writes them (rfx_scan_list_len): the merge first takes the top-k of the list
+ * heads and then admits only candidates above its k-th entry.  Any list_len gives the exact
+ * result; a wrong one only costs time. */
+int rfx_scan_list_len(rfx_index_t h, int64_t nq, int k, int* out_list_len);
+int rfx_topk_merge_lists(const float* cand_scores_d, const void* cand_rows_d, int rows_are_i64,
+                         int64_t nq, int64_t n_cand, int list_len, int k, int64_t row_offset,
+                         float* out_scores_d, int64_t* out_rows_d, void* stream);
+/* Multi-GPU exchange.  A rank's merged top-k as [nq][k] 16-byte records
+ * {f32 score, i32 pad, i64 global row} (row_offset added) — the buffer handed to the all-gather —
+ * and the merge of the gathered [world][nq][k] records into the final top-k.  Replaces nothing in
+ * the reference (it has no collective); the records are rfx/dist.py pack()'s layout. */
+int rfx_topk_merge_records(const float* cand_scores_d, const void* cand_rows_d, int rows_are_i64,
+                           int64_t nq, int64_t n_cand, int list_len, int k, int64_t row_offset,
+                           void* out_records_d, void* stream);
+int rfx_merge_gathered(const void* records_d, int world, int64_t nq, int k, float* out_scores_d,
+                       int64_t* out_rows_d, void* stream);
 
 /* ---- text → features (host) ---------------------------------------------------------------
  * The reference has no chunker/tokeniser of its own (chunking_config is forwarded to Gemini,

@@ -71,7 +71,7 @@ static_assert(kGPW == 2 && kTauGPW == 2, "DMA pieces per wave");
 // 512 = shared threshold table ignored, 1024 = no pruning bound at all, 2048 = threshold table
 // refreshed by a plain (L1) buffer LDS-DMA, 4096 = by global_load_lds sc1, 8192 = write each lane
 // list's final pruning bound instead of candidates, 16384 = stage-end wait drains vmcnt to 0,
-// 32768 = stage-end wait one stage stricter.
+// 32768 = stage-end wait one stage stricter, 65536 = write every list entry (no final bound).
 template <int DT, int KL, int D, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_mfma5_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Qp,
                                                             int nq, int ntiles, uint32_t* __restrict__ tau,
@@ -282,12 +282,24 @@ __global__ __launch_bounds__(512, 1) void scan_mfma5_kernel(const uint16_t* __re
     return;
   }
   if (q < nq) {
+    // Drop entries below the query's bound as it stands now, read fresh from the slot table (all
+    // workgroups end together, so it is close to final): valid bound => exact, and the merge then
+    // sees ~k live candidates per query instead of 512 lists.
+    uint32_t fin = thr;
+    if constexpr ((MODE & 65536) == 0) {
+      uint32_t m = 0xffffffffu;
+#pragma unroll
+      for (int j = 0; j < KL; ++j)
+        m = min(m, __hip_atomic_load(tau + (int64_t)q * kTauW + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      fin = max(fin, m);
+    }
     const int64_t o = ((int64_t)q * n_lists + lst) * KL;
 #pragma unroll
     for (int i = 0; i < KL; ++i) {
       const uint64_t key = Ls[i * 64];
-      cand_s[o + i] = key ? unord((uint32_t)(key >> 32)) : -__builtin_inff();
-      cand_r[o + i] = key ? (int)(~(uint32_t)key) : kEmptyRow;
+      const bool keep = key && (uint32_t)(key >> 32) >= fin;
+      cand_s[o + i] = keep ? unord((uint32_t)(key >> 32)) : -__builtin_inff();
+      cand_r[o + i] = keep ? (int)(~(uint32_t)key) : kEmptyRow;
     }
   }
 }

@@ -81,6 +81,7 @@ int launch_scan_mfma5_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
     RFX_K5_DBG(8192)
     RFX_K5_DBG(16384)
     RFX_K5_DBG(32768)
+    RFX_K5_DBG(65536)
     RFX_K5_DBG(257)
     default:
       return -1;

@@ -301,67 +301,220 @@ void launch_widen_queries(const void* Q, int64_t n, int dtype, float* out, hipSt
 }
 
 // ---------------------------------------------------------------------------------------
-// Top-k merge: one 512-thread block per query; each wave folds a strided share of the
-// candidates into a wave list, then wave 0 folds the other 7 lists (through LDS).
-// Candidates: [nq][n_cand] (score, row) with rows int32 (local) or int64 (global).
+// Top-k merge: one 512-thread block per query.  The candidates of a query are groups of
+// `list_len` (the scan kernels' sorted partial lists; list_len = 1: no structure).
+//   pass 1: the 8 waves fold the list HEADS (each list's first entry) into wave lists; wave 0
+//           merges them into H = top-K of the heads.  T = H's K-th entry.
+//   pass 2: every other candidate enters a wave list only if it beats T (one ballot per 64
+//           candidates; with sorted lists almost everything is rejected there).
+//   final:  wave 0 merges H and the 8 pass-2 lists.
+// Exact for any grouping: H holds K distinct candidates >= T, so every candidate of the final
+// top-K that is not a head beats T strictly (rows are distinct, ties break on the row id).
+// Sources: flat [nq][n_cand] (score, row) arrays, or the all-gathered per-rank records of the
+// multi-GPU path ([world][nq][k] of {f32 score, pad, i64 row}).
 // ---------------------------------------------------------------------------------------
-template <int K, bool R64>
-__global__ __launch_bounds__(512) void merge_kernel(const float* __restrict__ cs, const void* __restrict__ cr,
-                                                    int64_t n_cand, int k_out, int64_t row_offset,
-                                                    float* __restrict__ out_s, int64_t* __restrict__ out_r) {
-  __shared__ float ls_lds[8][K];
-  __shared__ long long lr_lds[8][K];
-  const int q = blockIdx.x;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const float* s = cs + (int64_t)q * n_cand;
+struct MergeRec {  // 16 B; the layout of rfx/dist.py pack(): int64(score bits) + int64 row
+  float s;
+  int pad;
+  long long r;
+};
+
+template <bool R64>
+struct FlatSrc {
+  const float* cs;
+  const void* cr;
+  int64_t n;  // candidates per query
+  __device__ __forceinline__ void get(int64_t q, int64_t i, float& s, long long& r) const {
+    s = cs[q * n + i];
+    if constexpr (R64)
+      r = ((const long long*)cr)[q * n + i];
+    else
+      r = (long long)((const int*)cr)[q * n + i];
+  }
+};
+struct GatheredSrc {
+  const MergeRec* rec;
+  int64_t nq;
+  int k;  // entries per rank (= list_len)
+  int64_t n;
+  __device__ __forceinline__ void get(int64_t q, int64_t i, float& s, long long& r) const {
+    const int64_t rank = i / k, e = i - rank * k;
+    const MergeRec m = rec[(rank * nq + q) * k + e];
+    s = m.s;
+    r = m.r;
+  }
+};
+
+constexpr long long kNoRow = 0x7fffffffffffffffll;
+
+// Fold candidates i = base + (p * 8 * 64) + lane, p < P, of one query into the wave list.  All P
+// loads are issued before the first offer, so a chunk costs one memory latency, not P.
+// `skip_heads`: candidates at list heads (i % list_len == 0) are not offered.
+template <int K, bool R64, int P, class Src>
+__device__ __forceinline__ void merge_chunk(const Src& src, int64_t q, int64_t base, int64_t n, int lane,
+                                            int list_len, bool skip_heads, WaveList64<K>& L) {
+  float sc[P];
+  long long rr[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const int64_t i = base + (int64_t)p * 8 * 64 + lane;
+    sc[p] = -__builtin_inff();
+    rr[p] = kNoRow;
+    if (i < n && !(skip_heads && i % list_len == 0)) src.get(q, i, sc[p], rr[p]);
+  }
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    // empty slots of partial lists carry a sentinel row: never valid candidates
+    const bool live = rr[p] >= 0 && rr[p] != kNoRow && (R64 || rr[p] != (long long)kEmptyRow);
+    L.offer(sc[p], rr[p], live);
+  }
+}
+
+// One head (list_len-strided candidate) per lane.
+template <int K, bool R64, class Src>
+__device__ __forceinline__ void merge_heads(const Src& src, int64_t q, int64_t nh, int list_len, int w, int lane,
+                                            WaveList64<K>& L) {
+  for (int64_t b = (int64_t)w * 64; b < nh; b += 8 * 64) {
+    const int64_t h = b + lane;
+    float sc = -__builtin_inff();
+    long long rr = kNoRow;
+    if (h < nh) src.get(q, h * list_len, sc, rr);
+    const bool live = rr >= 0 && rr != kNoRow && (R64 || rr != (long long)kEmptyRow);
+    L.offer(sc, rr, live);
+  }
+}
+
+// Block-wide merge of M sorted lists of K (best first, padded with (-inf, kNoRow)) in LDS into the
+// top-K list `dst` (pre-filled with padding by the caller): every thread takes candidates and
+// computes their rank as its index plus, for each other list, the number of entries better than
+// it (binary search).  The ranks of distinct (score, row) pairs are distinct, so each of the K
+// best lands in its own slot.  O(M log K) per candidate, no serial chain.
+template <int K, int M>
+__device__ __forceinline__ void rank_merge(const float (*ls)[K], const long long (*lr)[K], float* dst_s,
+                                           long long* dst_r) {
+  for (int t = threadIdx.x; t < M * K; t += blockDim.x) {
+    const int m = t / K, e = t - (t / K) * K;
+    const float s = ls[m][e];
+    const long long r = lr[m][e];
+    if (r == kNoRow) continue;
+    int rank = e;
+    for (int mm = 0; mm < M && rank < K; ++mm) {
+      if (mm == m) continue;
+      int lo = 0, hi = K;  // first entry of list mm that is not better than (s, r)
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (better64(ls[mm][mid], lr[mm][mid], s, r))
+          lo = mid + 1;
+        else
+          hi = mid;
+      }
+      rank += lo;
+    }
+    if (rank < K) {
+      dst_s[rank] = s;
+      dst_r[rank] = r;
+    }
+  }
+}
+
+template <int K, bool R64, class Src>
+__global__ __launch_bounds__(512) void merge_kernel(Src src, int list_len, int k_out, int64_t row_offset,
+                                                    float* __restrict__ out_s, int64_t* __restrict__ out_r,
+                                                    MergeRec* __restrict__ out_rec) {
+  // rows 0..7: wave lists, row 8: H (top-K of pass 1), row 9: final
+  __shared__ float ls_lds[10][K];
+  __shared__ long long lr_lds[10][K];
+  const int64_t q = blockIdx.x;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int64_t n = src.n;
+  const int64_t nh = list_len > 1 ? n / list_len : n;  // heads
+  constexpr int P = 8;  // chunk: 8 * 512 candidates per block
+  if (tid < 2 * K) {
+    ls_lds[8 + tid / K][tid % K] = -__builtin_inff();
+    lr_lds[8 + tid / K][tid % K] = kNoRow;
+  }
+  // ---- pass 1: heads (list_len == 1: every candidate is a head) ----
   WaveList64<K> L;
   L.init();
-  for (int64_t b = (int64_t)w * 64; b < n_cand; b += 8 * 64) {
-    const int64_t i = b + lane;
-    const bool valid = i < n_cand;
-    float sc = valid ? s[i] : -__builtin_inff();
-    long long rr;
-    if constexpr (R64)
-      rr = valid ? ((const long long*)cr)[(int64_t)q * n_cand + i] : 0x7fffffffffffffffll;
-    else
-      rr = valid ? (long long)((const int*)cr)[(int64_t)q * n_cand + i] : 0x7fffffffffffffffll;
-    // empty slots of partial lists carry the sentinel row: never valid candidates
-    const bool live = valid && rr >= 0 && rr != 0x7fffffffffffffffll && (R64 || rr != (long long)kEmptyRow);
-    L.offer(sc, rr, live);
+  if (list_len > 1) {
+    merge_heads<K, R64>(src, q, nh, list_len, w, lane, L);
+  } else {
+    for (int64_t base = (int64_t)w * 64; base < n; base += (int64_t)P * 8 * 64)
+      merge_chunk<K, R64, P>(src, q, base, n, lane, 1, false, L);
   }
   if (lane < K) {
     ls_lds[w][lane] = L.ls;
     lr_lds[w][lane] = L.lr;
   }
   __syncthreads();
-  if (w == 0) {
-    for (int ww = 1; ww < 8; ++ww) {
-      const bool valid = lane < K;
-      const float sc = valid ? ls_lds[ww][lane] : -__builtin_inff();
-      const long long rr = valid ? lr_lds[ww][lane] : 0x7fffffffffffffffll;
-      L.offer(sc, rr, valid && rr != 0x7fffffffffffffffll);
+  rank_merge<K, 8>(ls_lds, lr_lds, ls_lds[8], lr_lds[8]);  // H
+  __syncthreads();
+  int fin = 8;
+  // ---- pass 2: the rest, admitted only above T = H's K-th entry ----
+  if (list_len > 1) {
+    L.init_above(ls_lds[8][K - 1], lr_lds[8][K - 1]);
+    for (int64_t base = (int64_t)w * 64; base < n; base += (int64_t)P * 8 * 64)
+      merge_chunk<K, R64, P>(src, q, base, n, lane, list_len, true, L);
+    if (lane < K) {  // rows 0..7 were last read by the rank_merge above (a barrier ago)
+      ls_lds[w][lane] = L.ls;
+      lr_lds[w][lane] = L.lr;
     }
-    if (lane < k_out) {
-      const bool empty = L.lr == 0x7fffffffffffffffll;
-      out_s[(int64_t)q * k_out + lane] = empty ? -__builtin_inff() : L.ls;
-      out_r[(int64_t)q * k_out + lane] = empty ? -1 : L.lr + row_offset;
+    __syncthreads();
+    rank_merge<K, 9>(ls_lds, lr_lds, ls_lds[9], lr_lds[9]);
+    __syncthreads();
+    fin = 9;
+  }
+  if (tid < k_out) {
+    const long long rr = lr_lds[fin][tid];
+    const bool empty = rr == kNoRow;
+    const float s = empty ? -__builtin_inff() : ls_lds[fin][tid];
+    const long long r = empty ? -1 : rr + row_offset;
+    if (out_rec) {
+      out_rec[q * k_out + tid] = MergeRec{s, 0, r};
+    } else {
+      out_s[q * k_out + tid] = s;
+      out_r[q * k_out + tid] = r;
     }
   }
 }
 
-int launch_topk_merge(const float* cs, const void* cr, int rows_are_i64, int64_t nq, int64_t n_cand, int k,
-                      int64_t row_offset, float* out_s, int64_t* out_r, hipStream_t st) {
+int launch_topk_merge_lists(const float* cs, const void* cr, int rows_are_i64, int64_t nq, int64_t n_cand,
+                            int list_len, int k, int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec,
+                            hipStream_t st) {
   const int kk = valu_k_slot(k);
   if (nq <= 0) return 0;
-#define RFX_M(KV)                                                                                  \
-  if (kk == KV) {                                                                                  \
-    if (rows_are_i64)                                                                              \
-      hipLaunchKernelGGL((merge_kernel<KV, true>), dim3((unsigned)nq), dim3(512), 0, st, cs, cr,    \
-                         n_cand, k, row_offset, out_s, out_r);                                     \
-    else                                                                                           \
-      hipLaunchKernelGGL((merge_kernel<KV, false>), dim3((unsigned)nq), dim3(512), 0, st, cs, cr,   \
-                         n_cand, k, row_offset, out_s, out_r);                                     \
-    return 0;                                                                                      \
+  if (list_len < 1 || (list_len > 1 && n_cand % list_len != 0)) list_len = 1;
+  MergeRec* rec = (MergeRec*)out_rec;
+#define RFX_M(KV)                                                                                     \
+  if (kk == KV) {                                                                                     \
+    if (rows_are_i64)                                                                                 \
+      hipLaunchKernelGGL((merge_kernel<KV, true, FlatSrc<true>>), dim3((unsigned)nq), dim3(512), 0, st, \
+                         FlatSrc<true>{cs, cr, n_cand}, list_len, k, row_offset, out_s, out_r, rec);    \
+    else                                                                                              \
+      hipLaunchKernelGGL((merge_kernel<KV, false, FlatSrc<false>>), dim3((unsigned)nq), dim3(512), 0,   \
+                         st, FlatSrc<false>{cs, cr, n_cand}, list_len, k, row_offset, out_s, out_r, rec); \
+    return 0;                                                                                         \
+  }
+  RFX_VALU_K_LIST(RFX_M)
+#undef RFX_M
+  return -1;
+}
+
+int launch_topk_merge(const float* cs, const void* cr, int rows_are_i64, int64_t nq, int64_t n_cand, int k,
+                      int64_t row_offset, float* out_s, int64_t* out_r, hipStream_t st) {
+  return launch_topk_merge_lists(cs, cr, rows_are_i64, nq, n_cand, 1, k, row_offset, out_s, out_r, nullptr, st);
+}
+
+int launch_merge_gathered(const void* rec, int world, int64_t nq, int k, float* out_s, int64_t* out_r,
+                          hipStream_t st) {
+  const int kk = valu_k_slot(k);
+  if (nq <= 0) return 0;
+  GatheredSrc src{(const MergeRec*)rec, nq, k, (int64_t)world * k};
+#define RFX_M(KV)                                                                                     \
+  if (kk == KV) {                                                                                     \
+    hipLaunchKernelGGL((merge_kernel<KV, true, GatheredSrc>), dim3((unsigned)nq), dim3(512), 0, st, src, \
+                       k, k, 0, out_s, out_r, nullptr);                                               \
+    return 0;                                                                                         \
   }
   RFX_VALU_K_LIST(RFX_M)
 #undef RFX_M

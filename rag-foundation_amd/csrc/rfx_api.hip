@@ -499,6 +499,55 @@ int rfx_topk_merge(const float* cand_scores_d, const void* cand_rows_d, int rows
   return RFX_OK;
 }
 
+int rfx_scan_list_len(rfx_index_t h, int64_t nq, int k, int* out_list_len) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  if (!out_list_len) return fail(RFX_EINVAL, "null out");
+  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  SearchLayout L;
+  int rc = make_layout(*ix, nq, k, L);
+  if (rc) return rc;
+  *out_list_len = L.kernel ? L.mp.k_lane : L.vp.k_slot;
+  return RFX_OK;
+}
+
+int rfx_topk_merge_lists(const float* cand_scores_d, const void* cand_rows_d, int rows_are_i64, int64_t nq,
+                         int64_t n_cand, int list_len, int k, int64_t row_offset, float* out_scores_d,
+                         int64_t* out_rows_d, void* stream) {
+  if (k < 1 || k > 64) return fail(RFX_EINVAL, "k=%d out of range [1, 64]", k);
+  if (nq < 0 || n_cand < 0 || list_len < 1) return fail(RFX_EINVAL, "negative sizes / list_len < 1");
+  if (nq > 0 && (!out_scores_d || !out_rows_d)) return fail(RFX_EINVAL, "null outputs");
+  if (rfx::launch_topk_merge_lists(cand_scores_d, cand_rows_d, rows_are_i64, nq, n_cand, list_len, k, row_offset,
+                                   out_scores_d, out_rows_d, nullptr, (hipStream_t)stream) != 0)
+    return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
+int rfx_topk_merge_records(const float* cand_scores_d, const void* cand_rows_d, int rows_are_i64, int64_t nq,
+                           int64_t n_cand, int list_len, int k, int64_t row_offset, void* out_records_d,
+                           void* stream) {
+  if (k < 1 || k > 64) return fail(RFX_EINVAL, "k=%d out of range [1, 64]", k);
+  if (nq < 0 || n_cand < 0 || list_len < 1) return fail(RFX_EINVAL, "negative sizes / list_len < 1");
+  if (nq > 0 && !out_records_d) return fail(RFX_EINVAL, "null output");
+  if (rfx::launch_topk_merge_lists(cand_scores_d, cand_rows_d, rows_are_i64, nq, n_cand, list_len, k, row_offset,
+                                   nullptr, nullptr, out_records_d, (hipStream_t)stream) != 0)
+    return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
+int rfx_merge_gathered(const void* records_d, int world, int64_t nq, int k, float* out_scores_d, int64_t* out_rows_d,
+                       void* stream) {
+  if (k < 1 || k > 64) return fail(RFX_EINVAL, "k=%d out of range [1, 64]", k);
+  if (world < 1 || nq < 0) return fail(RFX_EINVAL, "world < 1 or nq < 0");
+  if (nq > 0 && (!records_d || !out_scores_d || !out_rows_d)) return fail(RFX_EINVAL, "null buffers");
+  if (rfx::launch_merge_gathered(records_d, world, nq, k, out_scores_d, out_rows_d, (hipStream_t)stream) != 0)
+    return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
 // Diagnostic entry point (not in include/rfx.h): the bf16 / nq 256 / k 10 MFMA scan with
 // parts of the kernel removed, for profiling (mode 1 = no top-k epilogue, 2 = no MFMA).
 int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k, int mode, float* cs, int32_t* cr,
@@ -514,7 +563,7 @@ int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k
   void* qpad = (uint8_t*)ws_d + L.q_off;
   rfx::launch_pad_queries(queries_d, nq, L.mp.nq_pad, ix->dim, 2, qpad, st);
   int rc2;
-  if (mode >= 1000 && mode < 100000)  // two-waves-per-SIMD kernel ablations: mode 1000 + MODE
+  if (mode >= 1000 && mode < 200000)  // two-waves-per-SIMD kernel ablations: mode 1000 + MODE
     rc2 = rfx::launch_scan_mfma5_dbg(rfx::plan_scan_mfma5(ix->rows, ix->dim, ix->dtype, nq, k), mode - 1000, ix->data,
                                      (int)ix->rows, ix->dtype, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st);
   else if (mode >= 20 && mode < 1000)  // all-query-stationary kernel ablations: mode 20 + MODE
@@ -561,7 +610,8 @@ int rfx_search(rfx_index_t h, const void* queries_d, int64_t nq, int k, float* o
   int32_t* cr = (int32_t*)(ws + L.cr_off);
   rc = scan_into(*ix, L, queries_d, nq, cs, cr, ws, st);
   if (rc) return rc;
-  if (rfx::launch_topk_merge(cs, cr, 0, nq, L.n_cand, k, 0, out_scores_d, out_rows_d, st) != 0)
+  const int list_len = L.kernel ? L.mp.k_lane : L.vp.k_slot;  // the scan writes sorted lists of this length
+  if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.n_cand, list_len, k, 0, out_scores_d, out_rows_d, nullptr, st) != 0)
     return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
   RFX_HIP(hipGetLastError());
   return RFX_OK;

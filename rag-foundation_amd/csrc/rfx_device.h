@@ -126,6 +126,13 @@ struct WaveList64 {
     tr = 0x7fffffffffffffffll;
   }
 
+  // empty list whose admission threshold is (s, r): only strictly better candidates enter
+  __device__ __forceinline__ void init_above(float s, long long r) {
+    init();
+    ts = s;
+    tr = r;
+  }
+
   __device__ __forceinline__ void offer(float cs, long long cr, bool valid) {
     const int lane = lane_id();
     uint64_t mask = __ballot(valid && better64(cs, cr, ts, tr));

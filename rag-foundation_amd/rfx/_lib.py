@@ -80,6 +80,10 @@ SIGNATURES = {
     "rfx_scan_plan": ([_u64, _i64, _i, _pi, _pi64], _i),
     "rfx_scan_topk": ([_u64, _p, _i64, _i, _p, _p, _p, _sz, _p], _i),
     "rfx_topk_merge": ([_p, _p, _i, _i64, _i64, _i, _i64, _p, _p, _p], _i),
+    "rfx_scan_list_len": ([_u64, _i64, _i, _p], _i),
+    "rfx_topk_merge_lists": ([_p, _p, _i, _i64, _i64, _i, _i, _i64, _p, _p, _p], _i),
+    "rfx_topk_merge_records": ([_p, _p, _i, _i64, _i64, _i, _i, _i64, _p, _p], _i),
+    "rfx_merge_gathered": ([_p, _i, _i64, _i, _p, _p, _p], _i),
     "rfx_chunk_whitespace": ([_p, _i64, _i, _i, _p, _i64, _pi64], _i),
     "rfx_featurize": ([_p, _p, _i64, _i, _u64, _p, _p, _p, _i64, _pi64], _i),
     "rfx_embed_weights": ([_i, _i, _u64, _p, _p], _i),

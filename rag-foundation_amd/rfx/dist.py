@@ -47,6 +47,20 @@ def gather_merge(local_s: torch.Tensor, local_r: torch.Tensor, k: int, merge, gr
     return merge(cs, cr, k)
 
 
+def gather_merge_records(records: torch.Tensor, k: int, group=None, stream=None):
+    """GPU path: all-gather this rank's [nq][k][2] int64 records (rfx.index.topk_merge_records,
+    rows already global) and merge the world's records with the HIP kernel.  Two device ops and
+    one collective per batch; no host-side tensor reshuffling."""
+    from .index import merge_gathered
+
+    world = dist.get_world_size(group)
+    if world == 1:
+        return merge_gathered(records.unsqueeze(0), k, stream=stream)
+    out = torch.empty((world,) + tuple(records.shape), dtype=records.dtype, device=records.device)
+    dist.all_gather_into_tensor(out, records, group=group)  # ranks concatenated along dim 0
+    return merge_gathered(out, k, stream=stream)
+
+
 class ShardedSearch:
     """Holds this rank's DeviceIndex shard and runs the global search."""
 
@@ -56,8 +70,10 @@ class ShardedSearch:
         self.group = group
 
     def search(self, queries: torch.Tensor, k: int, workspace=None, stream=None):
-        from .index import topk_merge
+        from .index import topk_merge_records
 
-        s, r = self.index.search(queries, k, workspace=workspace, stream=stream)
-        r = torch.where(r >= 0, r + self.row_offset, r)
-        return gather_merge(s, r, k, topk_merge, self.group)
+        nq = queries.shape[0]
+        cs, cr = self.index.scan(queries, k, workspace=workspace, stream=stream)
+        rec = topk_merge_records(cs, cr, k, row_offset=self.row_offset, stream=stream,
+                                 list_len=self.index.list_len(nq, k))
+        return gather_merge_records(rec, k, self.group, stream=stream)

@@ -136,6 +136,12 @@ class DeviceIndex:
                                  stream_ptr(stream)))
         return out_s, out_r
 
+    def list_len(self, nq: int, k: int) -> int:
+        """Length of the sorted candidate lists rfx_scan_topk writes (merge hint)."""
+        n = ctypes.c_int()
+        check(lib.rfx_scan_list_len(self.handle, int(nq), int(k), ctypes.byref(n)))
+        return n.value
+
     def plan(self, nq: int, k: int):
         kern, ncand = ctypes.c_int(), ctypes.c_int64()
         check(lib.rfx_scan_plan(self.handle, int(nq), int(k), ctypes.byref(kern), ctypes.byref(ncand)))
@@ -157,19 +163,55 @@ class DeviceIndex:
         return cs, cr
 
 
-def topk_merge(cand_s: torch.Tensor, cand_r: torch.Tensor, k: int, row_offset: int = 0, stream=None):
-    """Merge [nq][n_cand] candidates (rows int32 or int64) into the final top-k per query."""
+def _check_cands(cand_s: torch.Tensor, cand_r: torch.Tensor):
     if cand_s.shape != cand_r.shape or cand_s.dim() != 2:
         raise ValueError("candidate score/row tensors must be [nq][n_cand] of equal shape")
     if cand_r.dtype not in (torch.int32, torch.int64) or cand_s.dtype != torch.float32:
         raise ValueError("candidates must be (float32, int32|int64)")
-    cand_s, cand_r = cand_s.contiguous(), cand_r.contiguous()
+    return cand_s.contiguous(), cand_r.contiguous()
+
+
+def topk_merge(cand_s: torch.Tensor, cand_r: torch.Tensor, k: int, row_offset: int = 0, stream=None,
+               list_len: int = 1):
+    """Merge [nq][n_cand] candidates (rows int32 or int64) into the final top-k per query.
+    list_len: the candidates are sorted lists of that length (DeviceIndex.list_len); 1 = no hint."""
+    cand_s, cand_r = _check_cands(cand_s, cand_r)
     nq, ncand = cand_s.shape
     out_s = torch.empty((nq, k), dtype=torch.float32, device=cand_s.device)
     out_r = torch.empty((nq, k), dtype=torch.int64, device=cand_s.device)
     with torch.cuda.device(cand_s.device):
-        check(lib.rfx_topk_merge(ptr(cand_s), ptr(cand_r), int(cand_r.dtype == torch.int64), nq, ncand, int(k),
-                                 int(row_offset), ptr(out_s), ptr(out_r), stream_ptr(stream)))
+        check(lib.rfx_topk_merge_lists(ptr(cand_s), ptr(cand_r), int(cand_r.dtype == torch.int64), nq, ncand,
+                                       int(list_len), int(k), int(row_offset), ptr(out_s), ptr(out_r),
+                                       stream_ptr(stream)))
+    return out_s, out_r
+
+
+def topk_merge_records(cand_s: torch.Tensor, cand_r: torch.Tensor, k: int, row_offset: int = 0, stream=None,
+                       list_len: int = 1, out: torch.Tensor = None) -> torch.Tensor:
+    """Merge as topk_merge, writing [nq][k][2] int64 records (score bits, global row): the
+    all-gather input of the multi-GPU step (rfx.dist.pack's layout)."""
+    cand_s, cand_r = _check_cands(cand_s, cand_r)
+    nq, ncand = cand_s.shape
+    if out is None:
+        out = torch.empty((nq, k, 2), dtype=torch.int64, device=cand_s.device)
+    elif out.shape != (nq, k, 2) or out.dtype != torch.int64 or not out.is_contiguous():
+        raise ValueError(f"out must be a contiguous int64 [{nq}][{k}][2] tensor")
+    with torch.cuda.device(cand_s.device):
+        check(lib.rfx_topk_merge_records(ptr(cand_s), ptr(cand_r), int(cand_r.dtype == torch.int64), nq, ncand,
+                                         int(list_len), int(k), int(row_offset), ptr(out), stream_ptr(stream)))
+    return out
+
+
+def merge_gathered(gathered: torch.Tensor, k: int, stream=None):
+    """Final merge of all-gathered records [world][nq][k][2] int64 -> (scores [nq][k], rows [nq][k])."""
+    if gathered.dim() != 4 or gathered.shape[3] != 2 or gathered.dtype != torch.int64 or gathered.shape[2] != k:
+        raise ValueError("gathered must be int64 [world][nq][k][2]")
+    g = gathered.contiguous()
+    world, nq = g.shape[0], g.shape[1]
+    out_s = torch.empty((nq, k), dtype=torch.float32, device=g.device)
+    out_r = torch.empty((nq, k), dtype=torch.int64, device=g.device)
+    with torch.cuda.device(g.device):
+        check(lib.rfx_merge_gathered(ptr(g), int(world), nq, int(k), ptr(out_s), ptr(out_r), stream_ptr(stream)))
     return out_s, out_r
 
 

@@ -1,0 +1,136 @@
+"""GPU: the top-k merge kernels through the C ABI — list-structured merge (heads prefilter),
+packed all-gather records and the gathered merge of the multi-GPU step — against a numpy
+oracle merge (score desc, row asc; the tie rule of oracle/search.py)."""
+import numpy as np
+import pytest
+import torch
+
+from rfx import dist as rdist
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rindex():
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    import rfx.index as ri
+    return ri
+
+
+def oracle_merge(s, r, k):
+    """numpy reference: drop sentinel rows (< 0 or int32 max), sort by (-score, row)."""
+    nq = s.shape[0]
+    out_s = np.full((nq, k), -np.inf, dtype=np.float32)
+    out_r = np.full((nq, k), -1, dtype=np.int64)
+    for i in range(nq):
+        live = (r[i] >= 0) & (r[i] != 0x7fffffff) & (r[i] != 0x7fffffffffffffff)
+        order = np.lexsort((r[i][live], -s[i][live].astype(np.float64)))[:k]
+        out_s[i, :len(order)] = s[i][live][order]
+        out_r[i, :len(order)] = r[i][live][order]
+    return out_s, out_r
+
+
+def sorted_lists(rng, nq, n_lists, L, rows_total, empty_frac=0.1, ties=False):
+    """n_lists sorted lists of length L per query (best first), distinct rows, some empty tails."""
+    s = rng.standard_normal((nq, n_lists, L)).astype(np.float32)
+    if ties:
+        s = np.round(s * 8) / 8  # many equal scores: the row tie-break decides
+    s = -np.sort(-s, axis=2)
+    r = np.stack([rng.permutation(rows_total)[: n_lists * L] for _ in range(nq)]).reshape(nq, n_lists, L)
+    r = r.astype(np.int64)
+    if ties:  # within equal scores a list is ordered by row asc, as the scan writes it
+        for q in range(nq):
+            for j in range(n_lists):
+                o = np.lexsort((r[q, j], -s[q, j].astype(np.float64)))
+                s[q, j], r[q, j] = s[q, j][o], r[q, j][o]
+    cut = rng.random((nq, n_lists)) < empty_frac
+    for q, j in zip(*np.nonzero(cut)):
+        m = rng.integers(0, L)
+        s[q, j, m:] = -np.inf
+        r[q, j, m:] = 0x7fffffff
+    return s.reshape(nq, -1), r.reshape(nq, -1)
+
+
+@pytest.mark.parametrize("L,k", [(10, 10), (10, 5), (4, 4), (4, 1), (16, 16), (16, 12)])
+@pytest.mark.parametrize("ties", [False, True])
+def test_merge_lists_matches_oracle(rindex, L, k, ties):
+    rng = np.random.default_rng(L * 100 + k + ties)
+    s, r = sorted_lists(rng, 37, 512, L, 10_000_000, ties=ties)
+    ref_s, ref_r = oracle_merge(s, r, k)
+    cs = torch.from_numpy(s).cuda()
+    for rows_dtype in (torch.int32, torch.int64):
+        cr = torch.from_numpy(r).to(rows_dtype).cuda()
+        for ll in (L, 1):
+            out_s, out_r = rindex.topk_merge(cs, cr, k, list_len=ll)
+            assert np.array_equal(out_r.cpu().numpy(), ref_r), (ll, rows_dtype)
+            assert np.array_equal(out_s.cpu().numpy(), ref_s)
+
+
+def test_merge_lists_hint_on_unsorted_input_stays_exact(rindex):
+    """list_len is only a hint: on lists that are NOT sorted the result is still exact."""
+    rng = np.random.default_rng(3)
+    s = rng.standard_normal((16, 5120)).astype(np.float32)
+    r = np.stack([rng.permutation(1 << 20)[:5120] for _ in range(16)]).astype(np.int64)
+    ref_s, ref_r = oracle_merge(s, r, 10)
+    out_s, out_r = rindex.topk_merge(torch.from_numpy(s).cuda(), torch.from_numpy(r).cuda(), 10, list_len=10)
+    assert np.array_equal(out_r.cpu().numpy(), ref_r)
+
+
+def test_merge_row_offset_and_empty_queries(rindex):
+    s = np.full((3, 40), -np.inf, dtype=np.float32)
+    r = np.full((3, 40), 0x7fffffff, dtype=np.int64)
+    s[1, :4] = [0.5, 0.25, 0.125, 0.0]
+    r[1, :4] = [7, 3, 9, 1]
+    out_s, out_r = rindex.topk_merge(torch.from_numpy(s).cuda(), torch.from_numpy(r).to(torch.int32).cuda(), 5,
+                                     row_offset=1000, list_len=10)
+    out_r = out_r.cpu().numpy()
+    assert (out_r[0] == -1).all() and (out_r[2] == -1).all()
+    assert out_r[1].tolist() == [1007, 1003, 1009, 1001, -1]
+
+
+def test_merge_records_layout_is_dist_pack(rindex):
+    rng = np.random.default_rng(5)
+    s, r = sorted_lists(rng, 9, 64, 10, 1 << 20)
+    cs, cr = torch.from_numpy(s).cuda(), torch.from_numpy(r).to(torch.int32).cuda()
+    out_s, out_r = rindex.topk_merge(cs, cr, 10, row_offset=123, list_len=10)
+    rec = rindex.topk_merge_records(cs, cr, 10, row_offset=123, list_len=10)
+    ref = rdist.pack(out_s, out_r)
+    assert torch.equal(rec[..., 1], ref[..., 1])
+    assert torch.equal(rec[..., 0].to(torch.int32), ref[..., 0].to(torch.int32))  # score bits (low word)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_merge_gathered_equals_flat_merge(rindex, world):
+    """The multi-GPU exchange on one device: shards' records stacked as the all-gather lays them
+    out, merged by rfx_merge_gathered, equal the merge of every shard's candidates at once."""
+    rng = np.random.default_rng(world)
+    nq, k = 21, 10
+    shards = [sorted_lists(rng, nq, 32, 10, 1 << 20) for _ in range(world)]
+    recs = []
+    for w, (s, r) in enumerate(shards):
+        cs, cr = torch.from_numpy(s).cuda(), torch.from_numpy(r).to(torch.int32).cuda()
+        recs.append(rindex.topk_merge_records(cs, cr, k, row_offset=w * (1 << 20), list_len=10))
+    out_s, out_r = rindex.merge_gathered(torch.stack(recs), k)
+    all_s = np.concatenate([s for s, _ in shards], axis=1)
+    all_r = np.concatenate([np.where(r == 0x7fffffff, r, r + w * (1 << 20)) for w, (_, r) in enumerate(shards)], axis=1)
+    ref_s, ref_r = oracle_merge(all_s, all_r, k)
+    assert np.array_equal(out_r.cpu().numpy(), ref_r)
+    assert np.array_equal(out_s.cpu().numpy(), ref_s)
+
+
+def test_scan_then_records_then_gathered_equals_search(rindex):
+    """Sharded search on one device (2 shards of one corpus) == unsharded search."""
+    n, d = 40_000, 768
+    full = rindex.DeviceIndex(d, "bf16")
+    full.add_synthetic(11, n)
+    q = rindex.synth_rows(12, 0, 256, d, "bf16")
+    ref_s, ref_r = full.search(q, 10)
+    recs = []
+    for r0, r1 in (rdist.shard_range(n, 0, 2), rdist.shard_range(n, 1, 2)):
+        ix = rindex.DeviceIndex(d, "bf16")
+        ix.add_synthetic(11, r1 - r0, gen_row0=r0)
+        cs, cr = ix.scan(q, 10)
+        recs.append(rindex.topk_merge_records(cs, cr, 10, row_offset=r0, list_len=ix.list_len(256, 10)))
+    s, r = rindex.merge_gathered(torch.stack(recs), 10)
+    assert torch.equal(r, ref_r)
+    assert torch.equal(s, ref_s)
