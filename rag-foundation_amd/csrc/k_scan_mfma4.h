@@ -56,6 +56,17 @@ __device__ __forceinline__ v4f32x16 mfma(const uint4& a, const uint4& b, const v
                                                   0, 0, 0);
 }
 
+typedef __attribute__((ext_vector_type(4))) float v4f32x4;
+template <int DT>
+__device__ __forceinline__ v4f32x4 mfma16(const uint4& a, const uint4& b, const v4f32x4& c) {
+  if constexpr (DT == RFX_BF16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(v4bf16x8, a), __builtin_bit_cast(v4bf16x8, b),
+                                                   c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(v4f16x8, a), __builtin_bit_cast(v4f16x8, b), c,
+                                                  0, 0, 0);
+}
+
 __device__ __forceinline__ uint32_t ord(float f) {
   const uint32_t b = __float_as_uint(f);
   return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
@@ -152,8 +163,11 @@ __device__ __forceinline__ uint32_t tau_min(const uint8_t* p) {
 // both terms only grow, so the bound is kept as a running max.  The list is touched only when
 // some row of the tile reaches the bound; after such an update the list's best is published to
 // its slot (device atomicMax).
-template <int KL>
-__device__ __forceinline__ void fold(const v4f32x16& acc, uint64_t* Ls, uint32_t& thr_o, int rbase, v4i32 tau_rsrc,
+// ROWMAP 0: value r of the lane is row rbase + (r & 3) + 8 (r >> 2) (32x32 accumulator layout);
+// ROWMAP 1: row rbase + (r & 7) + 16 (r >> 3) (k_scan_mfma5.h's 16x16x32 pair-swapped layout).
+// V: anything with float operator[](int) over 16 values (a 32x32 accumulator, or Acc4View).
+template <int KL, int ROWMAP = 0, class V = v4f32x16>
+__device__ __forceinline__ void fold(const V& acc, uint64_t* Ls, uint32_t& thr_o, int rbase, v4i32 tau_rsrc,
                                      uint32_t slot_voff, int& n_slow) {
   float mx = max3f(acc[0], acc[1], acc[2]);
 #pragma unroll
@@ -168,7 +182,7 @@ __device__ __forceinline__ void fold(const v4f32x16& acc, uint64_t* Ls, uint32_t
     for (int r = 0; r < 16; ++r) {
       const float s = acc[r];
       if (s >= thr) {  // NaN (tombstoned rows, rows past the end) never passes
-        const int row = rbase + (r & 3) + 8 * (r >> 2);
+        const int row = ROWMAP == 0 ? rbase + (r & 3) + 8 * (r >> 2) : rbase + (r & 7) + 16 * (r >> 3);
         const uint64_t key = ((uint64_t)ord(s) << 32) | (uint32_t)(~(uint32_t)row);
         if (key > Ls[(KL - 1) * 64]) {
           int i = KL - 1;

@@ -82,6 +82,9 @@ int launch_scan_mfma5_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
     RFX_K5_DBG(16384)
     RFX_K5_DBG(32768)
     RFX_K5_DBG(65536)
+    RFX_K5_DBG(131072)
+    RFX_K5_DBG(131073)
+    RFX_K5_DBG(131081)
     RFX_K5_DBG(257)
     default:
       return -1;
