@@ -21,7 +21,7 @@
 //     32-row ds_read_b128 fragment reads (the permutation rides on the DMA source address).
 //   * per k-step and wave: 1 ds_read_b128 (32 rows × 16 k) → 1 v_mfma_f32_32x32x16.
 //   * top-k and the cross-workgroup pruning bound: as k_scan_mfma4.h (lane lists in LDS, per-query
-//     10-slot best-of-list table refreshed by DMA every 4 tiles) — one list per lane.
+//     10-slot best-of-list table refreshed by DMA, see tau_refresh_tile) — one list per lane.
 // Requires the index invariant of rfx_api.hip: rows [nrows, capacity) are NaN and capacity is a
 // multiple of 128, so the ragged last tile needs no clamping or masking.
 // Algorithmic bytes per tile: 32 * D * esize.
@@ -62,7 +62,12 @@ constexpr int kSlot = kTM * kRowB;        // 16 KB
 constexpr int kRing = 6;                  // 5 stages (80 KB) in flight
 constexpr int kGPW = kSlot / 1024 / kWaves;  // LDS-DMA wave-instructions per wave per stage (2)
 constexpr int kTauW = 16;                 // u32 per query in the threshold table (KL <= 10 used)
-constexpr int kTauEvery = 4;              // tiles between threshold refreshes
+// Threshold-table refreshes go out after the last stage of tiles 3, 7, 11, ... (16 KB of DMA each).
+// Measured: refreshing only every 16th tile after tile 31 made the kernel 20 % slower (a staler
+// bound sends more lanes into the insert path), so the table is refreshed every 4 tiles throughout.
+// (MODE 524288, diagnostic: every 2nd tile.  The vmcnt windows below allow refresh tiles >= 2 apart.)
+template <int MODE>
+__device__ __forceinline__ bool tau_refresh_tile(int it) { return (MODE & 524288) ? (it & 1) == 1 : (it & 3) == 3; }
 constexpr int kTauOff = kRing * kSlot;    // 96 KB
 constexpr int kTauBytes = kQG * kTauW * 4;  // 16 KB: 16 DMA wave-instructions, 2 per wave
 constexpr int kTauGPW = kTauBytes / 1024 / kWaves;
@@ -80,7 +85,8 @@ static_assert(kGPW == 2 && kTauGPW == 2, "DMA pieces per wave");
 // refreshed by a plain (L1) buffer LDS-DMA, 4096 = by global_load_lds sc1, 8192 = write each lane
 // list's final pruning bound instead of candidates, 16384 = stage-end wait drains vmcnt to 0,
 // 32768 = stage-end wait one stage stricter, 65536 = write every list entry (no final bound),
-// 131072 = v_mfma_f32_16x16x32 shape (S16).
+// 131072 = v_mfma_f32_16x16x32 shape (S16), 262144 = every other A fragment reused (half the LDS
+// reads; wrong scores, timing only).
 template <int DT, int KL, int D, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_mfma5_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Qp,
                                                             int nq, int ntiles, uint32_t* __restrict__ tau,
@@ -243,13 +249,13 @@ __global__ __launch_bounds__(512, 1) void scan_mfma5_kernel(const uint16_t* __re
       // refreshed threshold image (issued 2 tiles ago; any image value is a valid bound), read
       // before the tile's first MFMA while the accumulator is dead.
       if constexpr ((MODE & 512) == 0)
-        if ((it & (kTauEvery - 1)) == 1) thr = max(thr, tau_min<KL>(tq));
+        if (it >= 2 && tau_refresh_tile<MODE>(it - 2)) thr = max(thr, tau_min<KL>(tq));
     }
-    // A threshold refresh (kTauGPW ops) issued after the barrier of stage g_r = last stage of tile
-    // it_r ≡ 3 (mod 4) is younger than stage g+1's pieces iff g-4 <= g_r <= g-1: in tile it ≡ 0
-    // at every stage and in tile it ≡ 1 at stage 0, once such a refresh exists (it_r >= 3).
-    const bool tau_young12 = it >= kTauEvery && (it & (kTauEvery - 1)) == 0;
-    const bool tau_young0 = tau_young12 || (it > kTauEvery && (it & (kTauEvery - 1)) == 1);
+    // A threshold refresh (kTauGPW ops) issued after the barrier of stage g_r = last stage of a
+    // refresh tile it_r is younger than stage g+1's pieces iff g-4 <= g_r <= g-1: at every stage
+    // of tile it_r + 1 and at stage 0 of tile it_r + 2 (refresh tiles are >= 4 apart).
+    const bool tau_young12 = it >= 1 && tau_refresh_tile<MODE>(it - 1);
+    const bool tau_young0 = tau_young12 || (it >= 2 && tau_refresh_tile<MODE>(it - 2));
 #pragma unroll
     for (int s = 0; s < NST; ++s) {
       const int g = gbase + s;
@@ -278,7 +284,7 @@ __global__ __launch_bounds__(512, 1) void scan_mfma5_kernel(const uint16_t* __re
           }
           asm volatile("s_barrier" ::: "memory");
           if constexpr ((MODE & 8) == 0) {
-            if (s == NST - 1 && (it & (kTauEvery - 1)) == kTauEvery - 1) issue_tau();
+            if (s == NST - 1 && tau_refresh_tile<MODE>(it)) issue_tau();
             if constexpr (!kSpread) {
 #pragma unroll
               for (int u = 0; u < kGPW; ++u) issue_piece(g + kRing, slot, u);
@@ -287,7 +293,14 @@ __global__ __launch_bounds__(512, 1) void scan_mfma5_kernel(const uint16_t* __re
         }
         const int ks = s * KPS + kk;
         // prefetch k-step kk + PF (crossing into stage g+1 after the barrier)
-        fr[(ks + PF) % NF] = kk + PF < KPS ? read_frag(slot, kk + PF) : read_frag((g + 1) % kRing, kk + PF - KPS);
+        if constexpr ((MODE & 262144) != 0) {  // diagnostic: every other fragment reused, half the LDS reads
+          if ((ks & 1) == 0)
+            fr[(ks + PF) % NF] = fr[(ks + PF - 1) % NF];
+          else
+            fr[(ks + PF) % NF] = kk + PF < KPS ? read_frag(slot, kk + PF) : read_frag((g + 1) % kRing, kk + PF - KPS);
+        } else {
+          fr[(ks + PF) % NF] = kk + PF < KPS ? read_frag(slot, kk + PF) : read_frag((g + 1) % kRing, kk + PF - KPS);
+        }
         const Frag& cur = fr[ks % NF];
         if constexpr ((MODE & 2) == 0) {
           if constexpr (S16) {

@@ -338,7 +338,8 @@ struct GatheredSrc {
   int k;  // entries per rank (= list_len)
   int64_t n;
   __device__ __forceinline__ void get(int64_t q, int64_t i, float& s, long long& r) const {
-    const int64_t rank = i / k, e = i - rank * k;
+    const int ii = (int)i;  // n_cand < 2^31 (host check)
+    const int64_t rank = ii / k, e = ii - (ii / k) * k;
     const MergeRec m = rec[(rank * nq + q) * k + e];
     s = m.s;
     r = m.r;
@@ -360,7 +361,7 @@ __device__ __forceinline__ void merge_chunk(const Src& src, int64_t q, int64_t b
     const int64_t i = base + (int64_t)p * 8 * 64 + lane;
     sc[p] = -__builtin_inff();
     rr[p] = kNoRow;
-    if (i < n && !(skip_heads && i % list_len == 0)) src.get(q, i, sc[p], rr[p]);
+    if (i < n && !(skip_heads && (int)i % list_len == 0)) src.get(q, i, sc[p], rr[p]);  // (n < 2^31)
   }
 #pragma unroll
   for (int p = 0; p < P; ++p) {

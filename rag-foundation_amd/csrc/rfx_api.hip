@@ -516,6 +516,7 @@ int rfx_topk_merge_lists(const float* cand_scores_d, const void* cand_rows_d, in
                          int64_t* out_rows_d, void* stream) {
   if (k < 1 || k > 64) return fail(RFX_EINVAL, "k=%d out of range [1, 64]", k);
   if (nq < 0 || n_cand < 0 || list_len < 1) return fail(RFX_EINVAL, "negative sizes / list_len < 1");
+  if (n_cand >= INT32_MAX) return fail(RFX_EINVAL, "n_cand must be < 2^31");
   if (nq > 0 && (!out_scores_d || !out_rows_d)) return fail(RFX_EINVAL, "null outputs");
   if (rfx::launch_topk_merge_lists(cand_scores_d, cand_rows_d, rows_are_i64, nq, n_cand, list_len, k, row_offset,
                                    out_scores_d, out_rows_d, nullptr, (hipStream_t)stream) != 0)
@@ -529,6 +530,7 @@ int rfx_topk_merge_records(const float* cand_scores_d, const void* cand_rows_d, 
                            void* stream) {
   if (k < 1 || k > 64) return fail(RFX_EINVAL, "k=%d out of range [1, 64]", k);
   if (nq < 0 || n_cand < 0 || list_len < 1) return fail(RFX_EINVAL, "negative sizes / list_len < 1");
+  if (n_cand >= INT32_MAX) return fail(RFX_EINVAL, "n_cand must be < 2^31");
   if (nq > 0 && !out_records_d) return fail(RFX_EINVAL, "null output");
   if (rfx::launch_topk_merge_lists(cand_scores_d, cand_rows_d, rows_are_i64, nq, n_cand, list_len, k, row_offset,
                                    nullptr, nullptr, out_records_d, (hipStream_t)stream) != 0)
@@ -563,7 +565,7 @@ int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k
   void* qpad = (uint8_t*)ws_d + L.q_off;
   rfx::launch_pad_queries(queries_d, nq, L.mp.nq_pad, ix->dim, 2, qpad, st);
   int rc2;
-  if (mode >= 1000 && mode < 1000000)  // two-waves-per-SIMD kernel ablations: mode 1000 + MODE
+  if (mode >= 1000 && mode < 2000000)  // two-waves-per-SIMD kernel ablations: mode 1000 + MODE
     rc2 = rfx::launch_scan_mfma5_dbg(rfx::plan_scan_mfma5(ix->rows, ix->dim, ix->dtype, nq, k), mode - 1000, ix->data,
                                      (int)ix->rows, ix->dtype, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st);
   else if (mode >= 20 && mode < 1000)  // all-query-stationary kernel ablations: mode 20 + MODE
@@ -610,8 +612,9 @@ int rfx_search(rfx_index_t h, const void* queries_d, int64_t nq, int k, float* o
   int32_t* cr = (int32_t*)(ws + L.cr_off);
   rc = scan_into(*ix, L, queries_d, nq, cs, cr, ws, st);
   if (rc) return rc;
-  const int list_len = L.kernel ? L.mp.k_lane : L.vp.k_slot;  // the scan writes sorted lists of this length
-  if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.n_cand, list_len, k, 0, out_scores_d, out_rows_d, nullptr, st) != 0)
+  // one pass over all candidates: the list-heads prefilter (list_len > 1) measured slower on the
+  // scan's output (14 vs 19 us at 256 x 5120 candidates, tools/merge_bench.py)
+  if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.n_cand, 1, k, 0, out_scores_d, out_rows_d, nullptr, st) != 0)
     return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
   RFX_HIP(hipGetLastError());
   return RFX_OK;

@@ -72,8 +72,6 @@ class ShardedSearch:
     def search(self, queries: torch.Tensor, k: int, workspace=None, stream=None):
         from .index import topk_merge_records
 
-        nq = queries.shape[0]
         cs, cr = self.index.scan(queries, k, workspace=workspace, stream=stream)
-        rec = topk_merge_records(cs, cr, k, row_offset=self.row_offset, stream=stream,
-                                 list_len=self.index.list_len(nq, k))
+        rec = topk_merge_records(cs, cr, k, row_offset=self.row_offset, stream=stream)
         return gather_merge_records(rec, k, self.group, stream=stream)
