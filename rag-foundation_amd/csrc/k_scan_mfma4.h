@@ -117,6 +117,12 @@ __device__ __forceinline__ void bdma(v4i32 rsrc, uint32_t voff, uint32_t lds_add
                "s"(lds_addr)
                : "memory", "m0");
 }
+// Same with the non-temporal hint (a stream read once: no reuse to keep in the caches).
+__device__ __forceinline__ void bdma_nt(v4i32 rsrc, uint32_t voff, uint32_t lds_addr) {
+  asm volatile("s_nop 4\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen nt lds" ::"v"(voff),
+               "s"(rsrc), "s"(lds_addr)
+               : "memory", "m0");
+}
 // Same at device scope (sc1: misses this CU's L1, sees other workgroups' atomics).
 __device__ __forceinline__ void bdma_sc1(v4i32 rsrc, uint32_t voff, uint32_t lds_addr) {
   asm volatile("s_nop 4\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, 0 offen sc1 lds" ::"v"(voff),

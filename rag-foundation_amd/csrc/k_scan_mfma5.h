@@ -33,6 +33,7 @@ namespace k5 {
 
 using k4::batomic_umax;
 using k4::bdma;
+using k4::bdma_nt;
 using k4::bdma_sc1;
 using k4::fold;
 using k4::make_rsrc;
@@ -86,7 +87,8 @@ static_assert(kGPW == 2 && kTauGPW == 2, "DMA pieces per wave");
 // list's final pruning bound instead of candidates, 16384 = stage-end wait drains vmcnt to 0,
 // 32768 = stage-end wait one stage stricter, 65536 = write every list entry (no final bound),
 // 131072 = v_mfma_f32_16x16x32 shape (S16), 262144 = every other A fragment reused (half the LDS
-// reads; wrong scores, timing only).
+// reads; wrong scores, timing only), 524288 = threshold refresh every 2nd tile, 1048576 = corpus
+// DMA with the non-temporal hint.
 template <int DT, int KL, int D, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_mfma5_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Qp,
                                                             int nq, int ntiles, uint32_t* __restrict__ tau,
@@ -169,7 +171,10 @@ __global__ __launch_bounds__(512, 1) void scan_mfma5_kernel(const uint16_t* __re
     const int si = gi - ti * NST;
     const uint16_t* tbase = X + (int64_t)(range + ti * nblk) * kTM * D + si * kSK;
     const uint32_t dst = lds_base + (uint32_t)(slot * kSlot) + (uint32_t)((w + kWaves * u) * 1024);
-    bdma(make_rsrc(tbase), laneoff[u], __builtin_amdgcn_readfirstlane(dst));
+    if constexpr ((MODE & 1048576) != 0)
+      bdma_nt(make_rsrc(tbase), laneoff[u], __builtin_amdgcn_readfirstlane(dst));
+    else
+      bdma(make_rsrc(tbase), laneoff[u], __builtin_amdgcn_readfirstlane(dst));
   };
   // threshold table of the 256 queries -> LDS image (16 KB; wave w moves pieces w, w + 8)
   const v4i32 tau_rsrc = make_rsrc(tau);
