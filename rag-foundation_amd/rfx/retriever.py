@@ -8,6 +8,7 @@ from dataclasses import dataclass
 
 import torch
 
+from .batcher import GroupBatcher
 from .embedder import DEFAULT_MAX_TOKENS, DEFAULT_OVERLAP, Embedder
 from .store import registry as default_registry
 
@@ -33,24 +34,33 @@ def _chunking(cfg):
     return mt, min(ov, mt - 1)
 
 
+# Process-wide state: get_rag_client() builds a new adapter (and retriever) per request
+# (chat.py:937, ingestion.py:214), so embedders and batchers live at module level — one per
+# (device, dim) and per store — or no two requests would ever share a batch.
+_STATE_LOCK = threading.Lock()
+_EMBEDDERS = {}
+_BATCHERS = {}
+
+
 class GpuRetriever:
     def __init__(self, registry=None, dim=None, dtype=None):
         self._registry = registry
         self.dim = int(os.environ.get("RFX_DIM", "768")) if dim is None else int(dim)
         self.dtype = os.environ.get("RFX_DTYPE", "f32") if dtype is None else dtype
-        self._emb = {}
-        self._lock = threading.Lock()
+        # micro-batching of concurrent questions per store (RFX_BATCH=0 disables)
+        self.batching = os.environ.get("RFX_BATCH", "1") != "0"
 
     @property
     def registry(self):
         return self._registry or default_registry()
 
     def embedder(self, dim) -> Embedder:
-        with self._lock:
-            e = self._emb.get(dim)
+        key = (self.registry.device, dim)
+        with _STATE_LOCK:
+            e = _EMBEDDERS.get(key)
             if e is None:
                 e = Embedder(dim=dim, device=self.registry.device)
-                self._emb[dim] = e
+                _EMBEDDERS[key] = e
             return e
 
     # ---- store namespace ----------------------------------------------------------------------
@@ -58,6 +68,9 @@ class GpuRetriever:
         return self.registry.create(display_name, self.dim, self.dtype).name
 
     def drop_store(self, name):
+        with _STATE_LOCK:
+            for key in [k for k in _BATCHERS if k[0] == name]:
+                del _BATCHERS[key]
         return self.registry.drop(name)
 
     def store_names(self):
@@ -79,6 +92,31 @@ class GpuRetriever:
         return bool(st and st.delete_file(file_id))
 
     # ---- retrieval ----------------------------------------------------------------------------
+    def _search_store_batch(self, st, items):
+        """One GPU search for a batch of (question, k) against one store: one embedding GEMM,
+        one scan + merge at the largest k; each item gets its own first k."""
+        kmax = max(k for _, k in items)
+        with torch.cuda.device(st.device):
+            q = self.embedder(st.dim).embed_texts([t for t, _ in items], st.dtype)
+            s, r = st.index.search(q, kmax)
+            s, r = s.cpu().tolist(), r.cpu().tolist()
+        return [(s[i][:k], r[i][:k]) for i, (_, k) in enumerate(items)]
+
+    def _batcher(self, st):
+        key = (st.name, id(st))
+        with _STATE_LOCK:
+            b = _BATCHERS.get(key)
+            if b is None:
+                b = GroupBatcher(lambda items, st=st: self._search_store_batch(st, items), max_batch=256)
+                _BATCHERS[key] = b
+            return b
+
+    def search_store(self, st, question, k):
+        """(scores, rows) of one question against one store; batched with concurrent callers."""
+        if self.batching:
+            return self._batcher(st).submit((question, int(k)))
+        return self._search_store_batch(st, [(question, int(k))])[0]
+
     def search(self, store_names, question, k):
         """Top-k hits over the union of the named stores, rank order (score desc, store order,
         row asc)."""
@@ -87,10 +125,7 @@ class GpuRetriever:
             st = self.registry.get(name)
             if st is None or st.index.rows == 0:
                 continue
-            with torch.cuda.device(st.device):
-                q = self.embedder(st.dim).embed_texts([question], st.dtype)
-                s, r = st.index.search(q, k)
-                s, r = s.cpu().tolist()[0], r.cpu().tolist()[0]
+            s, r = self.search_store(st, question, k)
             for sc, row in zip(s, r):
                 if row < 0:
                     continue

@@ -405,3 +405,42 @@ def test_adapter_cfg1_end_to_end(rfx, golden_dir, tmp_path, monkeypatch):
     rag.delete_document_from_store(st, 1, "sample-report.md", file_id=up.file_id)
     assert rag.retrieve("mock-mode document assistant", [st]) == []
     rag.delete_store(st)
+
+
+def test_concurrent_retrieval_is_batched_and_equals_sequential(rfx, golden_dir, tmp_path):
+    """Micro-batching (rfx.batcher): 32 threads asking at once share GPU batches (fewer batches
+    than questions) and each gets the rows it gets alone."""
+    import threading
+
+    from rfx import retriever as rret
+    from rfx import store as rstore
+    from rfx.retriever import GpuRetriever
+
+    rstore.set_registry(rstore.StoreRegistry(root=str(tmp_path)))
+    ret = GpuRetriever(dtype="bf16")
+    st = ret.create_store("demo")
+    text = open(f"{golden_dir}/sample_report.md").read()
+    ret.add_document(st, text * 20, "doc", {"white_space_config": {"max_tokens_per_chunk": 5, "max_overlap_tokens": 1}})
+    words = text.split()
+    questions = [" ".join(words[i:i + 4]) for i in range(0, 4 * 32, 4)]
+    ret.batching = False
+    solo = [[(h.row, h.score) for h in ret.search([st], q, 5)] for q in questions]
+    ret.batching = True
+    out = [None] * len(questions)
+    gate = threading.Barrier(len(questions))
+
+    def ask(i):
+        gate.wait()
+        out[i] = [(h.row, h.score) for h in ret.search([st], questions[i], 5)]
+
+    th = [threading.Thread(target=ask, args=(i,)) for i in range(len(questions))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    # same rows in the same order; scores within the parity tolerance (a batch of 32 runs the MFMA
+    # scan, a lone question the VALU scan: different f32 summation order)
+    assert [[r for r, _ in o] for o in out] == [[r for r, _ in o] for o in solo]
+    assert max(abs(a[1] - b[1]) for o, so in zip(out, solo) for a, b in zip(o, so)) <= TOL
+    b = [v for k, v in rret._BATCHERS.items() if k[0] == st][0]
+    assert b.items == len(questions) and b.batches < len(questions)
