@@ -56,8 +56,14 @@ def gather_merge_records(records: torch.Tensor, k: int, group=None, stream=None)
     world = dist.get_world_size(group)
     if world == 1:
         return merge_gathered(records.unsqueeze(0), k, stream=stream)
+    if dist.get_backend(group) == "gloo":
+        # gloo moves host tensors (tests / hosts without RCCL): the exchange goes through host
+        # memory, the merge still runs on the device
+        parts = [torch.empty_like(records, device="cpu") for _ in range(world)]
+        dist.all_gather(parts, records.cpu(), group=group)
+        return merge_gathered(torch.stack(parts).to(records.device), k, stream=stream)
     out = torch.empty((world,) + tuple(records.shape), dtype=records.dtype, device=records.device)
-    dist.all_gather_into_tensor(out, records, group=group)  # ranks concatenated along dim 0
+    dist.all_gather_into_tensor(out, records, group=group)  # RCCL over xGMI; ranks along dim 0
     return merge_gathered(out, k, stream=stream)
 
 
