@@ -108,6 +108,18 @@ int rfx_scan_plan(rfx_index_t h, int64_t nq, int k, int* out_kernel /* 0 VALU, 1
                   int64_t* out_n_cand /* candidates per query */);
 int rfx_scan_topk(rfx_index_t h, const void* queries_d, int64_t nq, int k, float* cand_scores_d,
                   int32_t* cand_rows_d, void* ws_d, size_t ws_bytes, void* stream);
+/* Metadata-filtered search.  Replaces the metadata_filter that ask_stream
+ * accepts and forwards to Gemini (gemini_rag.py:463-469,517-551, validated at chat.py:295-335;
+ * the mock ignores it, gemini_rag.py:673-694).  row_mask_d: device bitmap, bit (r & 31) of
+ * word r >> 5 set = row r may be returned, at least (rows + 31) / 32 words (mask_words); one
+ * mask for all nq queries.  NULL = no filter (same as rfx_search / rfx_scan_topk).  The scan
+ * kernels apply it per tile in their epilogue, so the corpus is still read once. */
+int rfx_search_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d,
+                      int64_t mask_words, float* out_scores_d, int64_t* out_rows_d, void* ws_d,
+                      size_t ws_bytes, void* stream);
+int rfx_scan_topk_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k,
+                         const uint32_t* row_mask_d, int64_t mask_words, float* cand_scores_d,
+                         int32_t* cand_rows_d, void* ws_d, size_t ws_bytes, void* stream);
 /* Merge per-query candidate lists into the final top-k.  rows are int32 (rows_are_i64 = 0) or
  * int64 (1); row_offset is added to every returned row (shard base for multi-GPU). */
 int rfx_topk_merge(const float* cand_scores_d, const void* cand_rows_d, int rows_are_i64,

@@ -88,7 +88,7 @@ __global__ __launch_bounds__(512) void scan_mfma_kernel(const uint16_t* __restri
                                                         const uint16_t* __restrict__ Qp, int nq,
                                                         int tiles_per_block, int ntiles,
                                                         float* __restrict__ cand_s, int* __restrict__ cand_r,
-                                                        int64_t n_lists) {
+                                                        int64_t n_lists, const uint32_t* __restrict__ mask) {
   using G = MfmaGeom<BN>;
   __shared__ __attribute__((aligned(1024))) uint8_t lds[3 * G::STAGE_BYTES];
 
@@ -218,6 +218,14 @@ __global__ __launch_bounds__(512) void scan_mfma_kernel(const uint16_t* __restri
       // ---- epilogue: fold this tile's scores into the lane lists ----
       const int tile = t0 + st / nk;
       const int rbase = tile * kBM + wm * G::WROWS + 4 * half;
+      if (mask) {  // metadata filter (uniform branch): excluded rows -> NaN
+#pragma unroll
+        for (int m = 0; m < G::MS; ++m) {
+          const uint32_t bits = acc_row_bits(mask, rbase + m * 32, nrows);
+#pragma unroll
+          for (int n = 0; n < G::NS; ++n) mask_acc16(acc[m][n], bits);
+        }
+      }
 #pragma unroll
       for (int n = 0; n < G::NS; ++n) {
         float mx = -__builtin_inff();
@@ -306,13 +314,13 @@ void launch_pad_queries(const void* Q, int64_t nq, int64_t nq_pad, int D, int es
 
 template <int DT, int BN>
 static int launch_mfma_kl(const MfmaPlan& p, const uint16_t* X, int nrows, int D, const uint16_t* Qp, int nq,
-                          float* cs, int* cr, hipStream_t st) {
+                          float* cs, int* cr, hipStream_t st, const uint32_t* mask) {
   const int ntiles = (nrows + kBM - 1) / kBM;
   dim3 grid(p.blocks, p.q_blocks);
 #define RFX_KL(KV)                                                                                     \
   if (p.k_lane == KV) {                                                                                \
     hipLaunchKernelGGL((scan_mfma_kernel<DT, BN, KV>), grid, dim3(512), 0, st, X, nrows, D, Qp, nq,     \
-                       p.tiles_per_block, ntiles, cs, cr, p.n_lists);                                  \
+                       p.tiles_per_block, ntiles, cs, cr, p.n_lists, mask);                            \
     return 0;                                                                                          \
   }
   RFX_KL(4) RFX_KL(8) RFX_KL(10) RFX_KL(16)
@@ -322,10 +330,10 @@ static int launch_mfma_kl(const MfmaPlan& p, const uint16_t* X, int nrows, int D
 
 template <int DT>
 static int launch_mfma_bn(const MfmaPlan& p, const uint16_t* X, int nrows, int D, const uint16_t* Qp, int nq,
-                          float* cs, int* cr, hipStream_t st) {
-  if (p.bn == 64) return launch_mfma_kl<DT, 64>(p, X, nrows, D, Qp, nq, cs, cr, st);
-  if (p.bn == 128) return launch_mfma_kl<DT, 128>(p, X, nrows, D, Qp, nq, cs, cr, st);
-  return launch_mfma_kl<DT, 256>(p, X, nrows, D, Qp, nq, cs, cr, st);
+                          float* cs, int* cr, hipStream_t st, const uint32_t* mask) {
+  if (p.bn == 64) return launch_mfma_kl<DT, 64>(p, X, nrows, D, Qp, nq, cs, cr, st, mask);
+  if (p.bn == 128) return launch_mfma_kl<DT, 128>(p, X, nrows, D, Qp, nq, cs, cr, st, mask);
+  return launch_mfma_kl<DT, 256>(p, X, nrows, D, Qp, nq, cs, cr, st, mask);
 }
 
 int launch_scan_mfma_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, int D, const void* Qpad, int nq,
@@ -337,22 +345,22 @@ int launch_scan_mfma_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, 
   const uint16_t* Qh = (const uint16_t*)Qpad;
   if (mode == 1)
     hipLaunchKernelGGL((scan_mfma_kernel<RFX_BF16, 256, 10, 1>), grid, dim3(512), 0, st, Xh, nrows, D, Qh, nq,
-                       p.tiles_per_block, ntiles, cs, cr, p.n_lists);
+                       p.tiles_per_block, ntiles, cs, cr, p.n_lists, nullptr);
   else if (mode == 2)
     hipLaunchKernelGGL((scan_mfma_kernel<RFX_BF16, 256, 10, 2>), grid, dim3(512), 0, st, Xh, nrows, D, Qh, nq,
-                       p.tiles_per_block, ntiles, cs, cr, p.n_lists);
+                       p.tiles_per_block, ntiles, cs, cr, p.n_lists, nullptr);
   else
     hipLaunchKernelGGL((scan_mfma_kernel<RFX_BF16, 256, 10, 0>), grid, dim3(512), 0, st, Xh, nrows, D, Qh, nq,
-                       p.tiles_per_block, ntiles, cs, cr, p.n_lists);
+                       p.tiles_per_block, ntiles, cs, cr, p.n_lists, nullptr);
   return 0;
 }
 
 int launch_scan_mfma(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                     float* cs, int* cr, hipStream_t st) {
+                     float* cs, int* cr, hipStream_t st, const uint32_t* mask) {
   if (!p.ok) return -1;
   if (dtype == RFX_BF16)
-    return launch_mfma_bn<RFX_BF16>(p, (const uint16_t*)X, nrows, D, (const uint16_t*)Qpad, nq, cs, cr, st);
-  return launch_mfma_bn<RFX_F16>(p, (const uint16_t*)X, nrows, D, (const uint16_t*)Qpad, nq, cs, cr, st);
+    return launch_mfma_bn<RFX_BF16>(p, (const uint16_t*)X, nrows, D, (const uint16_t*)Qpad, nq, cs, cr, st, mask);
+  return launch_mfma_bn<RFX_F16>(p, (const uint16_t*)X, nrows, D, (const uint16_t*)Qpad, nq, cs, cr, st, mask);
 }
 
 }  // namespace rfx

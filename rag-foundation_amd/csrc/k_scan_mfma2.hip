@@ -89,7 +89,7 @@ __global__ __launch_bounds__(512) void scan_mfma2_kernel(const uint16_t* __restr
                                                          const uint16_t* __restrict__ Qp, int nq, int tiles_per_block,
                                                          int ntiles, uint32_t* __restrict__ tau,
                                                          float* __restrict__ cand_s, int* __restrict__ cand_r,
-                                                         int64_t n_lists) {
+                                                         int64_t n_lists, const uint32_t* __restrict__ mask) {
   __shared__ __attribute__((aligned(1024))) uint8_t lds[kLds];
 
   const int tid = threadIdx.x;
@@ -229,6 +229,14 @@ __global__ __launch_bounds__(512) void scan_mfma2_kernel(const uint16_t* __restr
       const int tile = t0 + st / nk;
       const int rbase = tile * kB2M + wm * 128 + 4 * half;
       const bool full_tile = tile * kB2M + kB2M <= nrows;
+      if (mask) {  // metadata filter (uniform branch): excluded rows -> NaN
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const uint32_t bits = acc_row_bits(mask, rbase + m * 32, nrows);
+#pragma unroll
+          for (int n = 0; n < 2; ++n) mask_acc16(acc[m][n], bits);
+        }
+      }
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
         float mx = -__builtin_inff();
@@ -322,7 +330,7 @@ int launch_scan_mfma2_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
 #define RFX_M2(MV)                                                                                        \
   if (mode == MV) {                                                                                       \
     hipLaunchKernelGGL((scan_mfma2_kernel<RFX_BF16, 10, MV>), grid, dim3(512), 0, st, Xh, nrows, D, Qh, nq, \
-                       p.tiles_per_block, ntiles, tau, cs, cr, p.n_lists);                                \
+                       p.tiles_per_block, ntiles, tau, cs, cr, p.n_lists, nullptr);                       \
     return 0;                                                                                             \
   }
   RFX_M2(0) RFX_M2(1) RFX_M2(2) RFX_M2(3) RFX_M2(4) RFX_M2(5) RFX_M2(6) RFX_M2(7)
@@ -331,7 +339,7 @@ int launch_scan_mfma2_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
 }
 
 int launch_scan_mfma2(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st) {
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask) {
   if (!p.ok) return -1;
   const int ntiles = (nrows + kB2M - 1) / kB2M;
   if (hipMemsetAsync(tau, 0, (size_t)p.nq_pad * sizeof(uint32_t), st) != hipSuccess) return -2;
@@ -341,7 +349,7 @@ int launch_scan_mfma2(const MfmaPlan& p, const void* X, int nrows, int D, int dt
 #define RFX_KL2(DTV, KV)                                                                                  \
   if (dtype == DTV && p.k_lane == KV) {                                                                   \
     hipLaunchKernelGGL((scan_mfma2_kernel<DTV, KV>), grid, dim3(512), 0, st, Xh, nrows, D, Qh, nq,         \
-                       p.tiles_per_block, ntiles, tau, cs, cr, p.n_lists);                                \
+                       p.tiles_per_block, ntiles, tau, cs, cr, p.n_lists, mask);                          \
     return 0;                                                                                             \
   }
   RFX_KL2(RFX_BF16, 4) RFX_KL2(RFX_BF16, 8) RFX_KL2(RFX_BF16, 10) RFX_KL2(RFX_BF16, 16)

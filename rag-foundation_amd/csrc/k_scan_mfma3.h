@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256, 1) void scan_mfma3_kernel(const uint16_t* __re
                                                             const uint16_t* __restrict__ Qp, int nq,
                                                             int tiles_per_block, int ntiles, uint32_t* __restrict__ tau,
                                                             float* __restrict__ cand_s, int* __restrict__ cand_r,
-                                                            int64_t n_lists) {
+                                                            int64_t n_lists, const uint32_t* __restrict__ mask) {
   constexpr int NKS = D / 16;      // 16-deep MFMA k-steps
   constexpr int NST = D / k3BK;    // stages per tile
   __shared__ __attribute__((aligned(1024))) uint8_t lds[k3Lds];
@@ -210,6 +210,10 @@ __global__ __launch_bounds__(256, 1) void scan_mfma3_kernel(const uint16_t* __re
 
     // ---- epilogue: fold this tile's 256 rows into the lane list ----
     const int rbase = tile * k3M + 4 * half;
+    if (mask) {  // metadata filter (uniform branch): excluded rows -> NaN
+#pragma unroll
+      for (int m = 0; m < 4; ++m) mask_acc16(acc[m], acc_row_bits(mask, rbase + m * 32, nrows));
+    }
     float mx = -__builtin_inff();
 #pragma unroll
     for (int m = 0; m < 4; ++m)
@@ -254,16 +258,17 @@ __global__ __launch_bounds__(256, 1) void scan_mfma3_kernel(const uint16_t* __re
 // one translation unit per (dtype, D) instantiates the kernel for the lane-list sizes KL in {4, 10, 16}
 #define RFX_K3_INSTANTIATE(DTV, DV, NAME)                                                                  \
   int NAME(int kl, dim3 grid, hipStream_t st, const uint16_t* X, int nrows, const uint16_t* Qp, int nq,      \
-           int tiles_per_block, int ntiles, uint32_t* tau, float* cs, int* cr, int64_t n_lists) {          \
+           int tiles_per_block, int ntiles, uint32_t* tau, float* cs, int* cr, int64_t n_lists,            \
+           const uint32_t* mask) {                                                                         \
     if (kl == 4)                                                                                         \
       hipLaunchKernelGGL((scan_mfma3_kernel<DTV, 4, DV>), grid, dim3(256), 0, st, X, nrows, Qp, nq,        \
-                         tiles_per_block, ntiles, tau, cs, cr, n_lists);                                 \
+                         tiles_per_block, ntiles, tau, cs, cr, n_lists, mask);                           \
     else if (kl == 10)                                                                                   \
       hipLaunchKernelGGL((scan_mfma3_kernel<DTV, 10, DV>), grid, dim3(256), 0, st, X, nrows, Qp, nq,       \
-                         tiles_per_block, ntiles, tau, cs, cr, n_lists);                                 \
+                         tiles_per_block, ntiles, tau, cs, cr, n_lists, mask);                           \
     else if (kl == 16)                                                                                   \
       hipLaunchKernelGGL((scan_mfma3_kernel<DTV, 16, DV>), grid, dim3(256), 0, st, X, nrows, Qp, nq,       \
-                         tiles_per_block, ntiles, tau, cs, cr, n_lists);                                 \
+                         tiles_per_block, ntiles, tau, cs, cr, n_lists, mask);                           \
     else                                                                                                 \
       return -1;                                                                                         \
     return 0;                                                                                            \

@@ -6,7 +6,8 @@ namespace rfx {
 namespace k3 {
 #define RFX_K3_DECL(NAME)                                                                                  \
   int NAME(int kl, dim3 grid, hipStream_t st, const uint16_t* X, int nrows, const uint16_t* Qp, int nq,      \
-           int tiles_per_block, int ntiles, uint32_t* tau, float* cs, int* cr, int64_t n_lists);
+           int tiles_per_block, int ntiles, uint32_t* tau, float* cs, int* cr, int64_t n_lists,            \
+           const uint32_t* mask);
 RFX_K3_DECL(launch_bf16_768)
 RFX_K3_DECL(launch_bf16_1024)
 RFX_K3_DECL(launch_f16_768)
@@ -35,7 +36,7 @@ MfmaPlan plan_scan_mfma3(int64_t nrows, int D, int dtype, int64_t nq, int k) {
 }
 
 int launch_scan_mfma3(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st) {
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask) {
   if (!p.ok) return -1;
   const int ntiles = (nrows + k3::kM - 1) / k3::kM;
   if (hipMemsetAsync(tau, 0, (size_t)(p.nq_pad + 256) * sizeof(uint32_t), st) != hipSuccess) return -2;
@@ -44,7 +45,7 @@ int launch_scan_mfma3(const MfmaPlan& p, const void* X, int nrows, int D, int dt
   const uint16_t* Qh = (const uint16_t*)Qpad;
   auto f = dtype == RFX_BF16 ? (D == 768 ? k3::launch_bf16_768 : k3::launch_bf16_1024)
                              : (D == 768 ? k3::launch_f16_768 : k3::launch_f16_1024);
-  return f(p.k_lane, grid, st, Xh, nrows, Qh, nq, p.tiles_per_block, ntiles, tau, cs, cr, p.n_lists);
+  return f(p.k_lane, grid, st, Xh, nrows, Qh, nq, p.tiles_per_block, ntiles, tau, cs, cr, p.n_lists, mask);
 }
 
 }  // namespace rfx

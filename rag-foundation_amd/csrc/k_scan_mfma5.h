@@ -89,11 +89,14 @@ static_assert(kGPW == 2 && kTauGPW == 2, "DMA pieces per wave");
 // 131072 = v_mfma_f32_16x16x32 shape (S16), 262144 = every other A fragment reused (half the LDS
 // reads; wrong scores, timing only), 524288 = threshold refresh every 2nd tile, 1048576 = corpus
 // DMA with the non-temporal hint.
+// MODE bit for the row-masked (metadata-filter) production variant; all other bits are ablations
+constexpr int kModeMask = 2097152;
+
 template <int DT, int KL, int D, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_mfma5_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Qp,
                                                             int nq, int ntiles, uint32_t* __restrict__ tau,
                                                             float* __restrict__ cand_s, int* __restrict__ cand_r,
-                                                            int64_t n_lists) {
+                                                            int64_t n_lists, const uint32_t* __restrict__ mask) {
   // S16: v_mfma_f32_16x16x32 (2 row blocks × 2 query blocks per 32-deep k-step) instead of one
   // v_mfma_f32_32x32x16 per 16-deep k-step: same LDS bytes and MFMA cycles per FLOP; the chip holds
   // a higher clock on it with random operands (MI355X_MICROARCH.md 'DVFS give-back' item 7).
@@ -351,10 +354,13 @@ __global__ __launch_bounds__(512, 1) void scan_mfma5_kernel(const uint16_t* __re
       const int rbase = S16 ? tile * kTM + 8 * half : tile * kTM + 4 * half;
       uint32_t t0 = 0u;  // MODE 1024 (diagnostic): no pruning bound at all
       uint32_t& bound = (MODE & 1024) != 0 ? t0 : thr;
-      if constexpr (S16)
+      if constexpr (S16) {
         fold<KL, 1>(Acc4View{acc4}, Ls, bound, rbase, tau_rsrc, slot_voff, n_slow);
-      else
+      } else {
+        // metadata filter: one mask word per 32-row tile (uniform load); excluded rows -> NaN
+        if constexpr ((MODE & kModeMask) != 0) mask_acc16(acc, mask[tile] >> (4 * half));
         fold<KL, 0>(acc, Ls, bound, rbase, tau_rsrc, slot_voff, n_slow);
+      }
     } else {
       if (acc[0] == 12345.f) Ls[0] = 1;  // keep the MFMAs live
     }
@@ -395,13 +401,19 @@ __global__ __launch_bounds__(512, 1) void scan_mfma5_kernel(const uint16_t* __re
 // one translation unit per (dtype, D) instantiates the kernel for the lane-list sizes KL in {4, 10}
 #define RFX_K5_INSTANTIATE(DTV, DV, NAME)                                                                  \
   int NAME(int kl, dim3 grid, hipStream_t st, const uint16_t* X, const uint16_t* Qp, int nq, int ntiles,     \
-           uint32_t* tau, float* cs, int* cr, int64_t n_lists) {                                           \
-    if (kl == 4)                                                                                         \
+           uint32_t* tau, float* cs, int* cr, int64_t n_lists, const uint32_t* mask) {                      \
+    if (kl == 4 && !mask)                                                                                \
       hipLaunchKernelGGL((scan_mfma5_kernel<DTV, 4, DV>), grid, dim3(512), 0, st, X, Qp, nq, ntiles, tau, cs, \
-                         cr, n_lists);                                                                    \
-    else if (kl == 10)                                                                                   \
+                         cr, n_lists, mask);                                                              \
+    else if (kl == 10 && !mask)                                                                          \
       hipLaunchKernelGGL((scan_mfma5_kernel<DTV, 10, DV>), grid, dim3(512), 0, st, X, Qp, nq, ntiles, tau,  \
-                         cs, cr, n_lists);                                                                \
+                         cs, cr, n_lists, mask);                                                          \
+    else if (kl == 4)                                                                                    \
+      hipLaunchKernelGGL((scan_mfma5_kernel<DTV, 4, DV, kModeMask>), grid, dim3(512), 0, st, X, Qp, nq,     \
+                         ntiles, tau, cs, cr, n_lists, mask);                                             \
+    else if (kl == 10)                                                                                   \
+      hipLaunchKernelGGL((scan_mfma5_kernel<DTV, 10, DV, kModeMask>), grid, dim3(512), 0, st, X, Qp, nq,    \
+                         ntiles, tau, cs, cr, n_lists, mask);                                             \
     else                                                                                                 \
       return -1;                                                                                         \
     return 0;                                                                                            \

@@ -6,7 +6,7 @@ namespace rfx {
 namespace k5 {
 #define RFX_K5_DECL(NAME)                                                                                 \
   int NAME(int kl, dim3 grid, hipStream_t st, const uint16_t* X, const uint16_t* Qp, int nq, int ntiles,     \
-           uint32_t* tau, float* cs, int* cr, int64_t n_lists);
+           uint32_t* tau, float* cs, int* cr, int64_t n_lists, const uint32_t* mask);
 RFX_K5_DECL(launch_bf16_768)
 RFX_K5_DECL(launch_f16_768)
 #undef RFX_K5_DECL
@@ -37,13 +37,13 @@ MfmaPlan plan_scan_mfma5(int64_t nrows, int D, int dtype, int64_t nq, int k) {
 }
 
 int launch_scan_mfma5(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st) {
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask) {
   if (!p.ok || D != 768) return -1;
   const int ntiles = (nrows + k5::kTM - 1) / k5::kTM;
   if (hipMemsetAsync(tau, 0, tau_bytes_mfma5(p), st) != hipSuccess) return -2;
   dim3 grid(p.blocks, p.q_blocks);
   auto f = dtype == RFX_BF16 ? k5::launch_bf16_768 : k5::launch_f16_768;
-  return f(p.k_lane, grid, st, (const uint16_t*)X, (const uint16_t*)Qpad, nq, ntiles, tau, cs, cr, p.n_lists);
+  return f(p.k_lane, grid, st, (const uint16_t*)X, (const uint16_t*)Qpad, nq, ntiles, tau, cs, cr, p.n_lists, mask);
 }
 
 // Profiling ablations (bf16, d 768, KL 10), MODE bit flags of scan_mfma5_kernel:
@@ -53,7 +53,7 @@ int launch_scan_mfma5(const MfmaPlan& p, const void* X, int nrows, int D, int dt
 int launch_scan_mfma5_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, int dtype, const void* Qpad, int nq,
                           uint32_t* tau, float* cs, int* cr, hipStream_t st) {
   if (!p.ok) return -1;
-  if (mode == 0) return launch_scan_mfma5(p, X, nrows, 768, dtype, Qpad, nq, tau, cs, cr, st);  // production plan
+  if (mode == 0) return launch_scan_mfma5(p, X, nrows, 768, dtype, Qpad, nq, tau, cs, cr, st, nullptr);  // production plan
   if (p.k_lane != 10) return -1;
   const int ntiles = (nrows + k5::kTM - 1) / k5::kTM;
   if (hipMemsetAsync(tau, 0, tau_bytes_mfma5(p), st) != hipSuccess) return -2;
@@ -63,7 +63,7 @@ int launch_scan_mfma5_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
 #define RFX_K5_DBG(M)                                                                                  \
   case M:                                                                                              \
     hipLaunchKernelGGL((k5::scan_mfma5_kernel<RFX_BF16, 10, 768, M>), grid, dim3(512), 0, st, Xh, Qh, nq, \
-                       ntiles, tau, cs, cr, p.n_lists);                                                \
+                       ntiles, tau, cs, cr, p.n_lists, nullptr);                                       \
     break;
   switch (mode) {
     RFX_K5_DBG(0)

@@ -105,7 +105,8 @@ template <int DT, int NQT, int K, int VPL>
 __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restrict__ X, int nrows, int D,
                                                         const float* __restrict__ Qf, int nq,
                                                         int rows_per_wave, float* __restrict__ cand_s,
-                                                        int* __restrict__ cand_r, int n_lists) {
+                                                        int* __restrict__ cand_r, int n_lists,
+                                                        const uint32_t* __restrict__ mask) {
   constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
   constexpr int EPV = 16 / ESZ;
   extern __shared__ __attribute__((aligned(16))) float q_lds[];  // [NQT][D]
@@ -180,8 +181,10 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
       }
     }
     const int crow = base + j * 4 + g;
+    // metadata filter: rows whose mask bit is clear are never offered
+    const bool ok = crow < we && (mask == nullptr || row_allowed(mask, crow));
 #pragma unroll
-    for (int qi = 0; qi < NQT; ++qi) L[qi].offer(cand[qi], crow, crow < we);
+    for (int qi = 0; qi < NQT; ++qi) L[qi].offer(cand[qi], crow, ok);
   }
 
   if (lane < K) {
@@ -202,11 +205,12 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
 
 template <int DT, int NQT, int K>
 static int launch_valu_vpl(int vpl, dim3 grid, size_t lds, hipStream_t st, const uint8_t* X, int nrows,
-                           int D, const float* Qf, int nq, int rpw, float* cs, int* cr, int n_lists) {
+                           int D, const float* Qf, int nq, int rpw, float* cs, int* cr, int n_lists,
+                           const uint32_t* mask) {
 #define RFX_L(V)                                                                                  \
   if (vpl <= V) {                                                                                 \
     hipLaunchKernelGGL((scan_valu_kernel<DT, NQT, K, V>), grid, dim3(256), lds, st, X, nrows, D, Qf, \
-                       nq, rpw, cs, cr, n_lists);                                                 \
+                       nq, rpw, cs, cr, n_lists, mask);                                           \
     return 0;                                                                                     \
   }
   RFX_L(4) RFX_L(8) RFX_L(12) RFX_L(16)
@@ -217,9 +221,9 @@ static int launch_valu_vpl(int vpl, dim3 grid, size_t lds, hipStream_t st, const
 template <int DT, int NQT>
 static int launch_valu_k(int kk, int vpl, dim3 grid, size_t lds, hipStream_t st, const uint8_t* X,
                          int nrows, int D, const float* Qf, int nq, int rpw, float* cs, int* cr,
-                         int n_lists) {
+                         int n_lists, const uint32_t* mask) {
 #define RFX_K(KV) \
-  if (kk == KV) return launch_valu_vpl<DT, NQT, KV>(vpl, grid, lds, st, X, nrows, D, Qf, nq, rpw, cs, cr, n_lists);
+  if (kk == KV) return launch_valu_vpl<DT, NQT, KV>(vpl, grid, lds, st, X, nrows, D, Qf, nq, rpw, cs, cr, n_lists, mask);
   RFX_VALU_K_LIST(RFX_K)
 #undef RFX_K
   return -1;
@@ -249,7 +253,7 @@ ValuPlan plan_scan_valu(int64_t nrows, int D, int dtype, int64_t nq, int k) {
 }
 
 int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dtype, const float* Qf,
-                     int nq, float* cs, int* cr, hipStream_t st) {
+                     int nq, float* cs, int* cr, hipStream_t st, const uint32_t* mask) {
   dim3 grid(p.blocks, p.q_slices);
   const size_t lds = (size_t)p.nqt * D * sizeof(float);
   const uint8_t* Xb = (const uint8_t*)X;
@@ -257,12 +261,12 @@ int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dty
   if (p.nqt == NQV) {                                                                              \
     if (dtype == RFX_F32)                                                                          \
       return launch_valu_k<RFX_F32, NQV>(p.k_slot, p.vpl, grid, lds, st, Xb, nrows, D, Qf, nq,       \
-                                         p.rows_per_wave, cs, cr, p.n_lists);                      \
+                                         p.rows_per_wave, cs, cr, p.n_lists, mask);                      \
     if (dtype == RFX_BF16)                                                                         \
       return launch_valu_k<RFX_BF16, NQV>(p.k_slot, p.vpl, grid, lds, st, Xb, nrows, D, Qf, nq,      \
-                                          p.rows_per_wave, cs, cr, p.n_lists);                     \
+                                          p.rows_per_wave, cs, cr, p.n_lists, mask);                     \
     return launch_valu_k<RFX_F16, NQV>(p.k_slot, p.vpl, grid, lds, st, Xb, nrows, D, Qf, nq,         \
-                                       p.rows_per_wave, cs, cr, p.n_lists);                        \
+                                       p.rows_per_wave, cs, cr, p.n_lists, mask);                        \
   }
   RFX_NQ(1) RFX_NQ(4) RFX_NQ(8)
 #undef RFX_NQ

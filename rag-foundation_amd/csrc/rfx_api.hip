@@ -163,24 +163,27 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
 // query staging and thresholds live in the front of ws (q_off, tau_off < cs_off)
 size_t scan_ws_bytes(const SearchLayout& L) { return L.cs_off; }
 
+// mask: optional row mask on the device (metadata filter), (rows + 31) / 32 words, checked by the
+// caller; every production scan kernel applies it in its epilogue.
 int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq, float* cs, int32_t* cr,
-              uint8_t* ws, hipStream_t st) {
+              uint8_t* ws, hipStream_t st, const uint32_t* mask = nullptr) {
   if (ix.rows == 0 || nq == 0) return RFX_OK;
+  if (mask && L.kernel == 4) return fail(RFX_EUNSUPPORTED, "kernel 4 (ablation only) has no row-mask variant");
   if (L.kernel >= 1) {
     void* qpad = ws + L.q_off;
     rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, 2, qpad, st);
     uint32_t* tau = (uint32_t*)(ws + L.tau_off);
     const int rc =
-        L.kernel == 5 ? rfx::launch_scan_mfma5(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
+        L.kernel == 5 ? rfx::launch_scan_mfma5(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
         : L.kernel == 4 ? rfx::launch_scan_mfma4(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
-        : L.kernel == 3 ? rfx::launch_scan_mfma3(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
-        : L.kernel == 2 ? rfx::launch_scan_mfma2(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
-                        : rfx::launch_scan_mfma(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, cs, cr, st);
+        : L.kernel == 3 ? rfx::launch_scan_mfma3(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
+        : L.kernel == 2 ? rfx::launch_scan_mfma2(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
+                        : rfx::launch_scan_mfma(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, cs, cr, st, mask);
     if (rc != 0) return fail(RFX_EUNSUPPORTED, "MFMA scan launch rejected (%d)", rc);
   } else {
     float* qf = (float*)(ws + L.q_off);
     rfx::launch_widen_queries(queries, nq * ix.dim, ix.dtype, qf, st);
-    if (rfx::launch_scan_valu(L.vp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qf, (int)nq, cs, cr, st) != 0)
+    if (rfx::launch_scan_valu(L.vp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qf, (int)nq, cs, cr, st, mask) != 0)
       return fail(RFX_EUNSUPPORTED, "VALU scan launch rejected");
   }
   RFX_HIP(hipGetLastError());
@@ -475,6 +478,12 @@ int rfx_scan_plan(rfx_index_t h, int64_t nq, int k, int* out_kernel, int64_t* ou
 
 int rfx_scan_topk(rfx_index_t h, const void* queries_d, int64_t nq, int k, float* cand_scores_d,
                   int32_t* cand_rows_d, void* ws_d, size_t ws_bytes, void* stream) {
+  return rfx_scan_topk_masked(h, queries_d, nq, k, nullptr, 0, cand_scores_d, cand_rows_d, ws_d, ws_bytes, stream);
+}
+
+int rfx_scan_topk_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d,
+                         int64_t mask_words, float* cand_scores_d, int32_t* cand_rows_d, void* ws_d, size_t ws_bytes,
+                         void* stream) {
   auto ix = get(h);
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
   std::shared_lock<std::shared_mutex> lk(ix->mu);
@@ -483,8 +492,11 @@ int rfx_scan_topk(rfx_index_t h, const void* queries_d, int64_t nq, int k, float
   if (rc) return rc;
   if (ws_bytes < scan_ws_bytes(L) || !ws_d) return fail(RFX_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, scan_ws_bytes(L));
   if (nq > 0 && !queries_d) return fail(RFX_EINVAL, "null queries");
+  if (row_mask_d && mask_words < (ix->rows + 31) / 32)
+    return fail(RFX_EINVAL, "row mask has %lld words, the index needs %lld", (long long)mask_words,
+                (long long)((ix->rows + 31) / 32));
   RFX_HIP(hipSetDevice(ix->device));
-  return scan_into(*ix, L, queries_d, nq, cand_scores_d, cand_rows_d, (uint8_t*)ws_d, (hipStream_t)stream);
+  return scan_into(*ix, L, queries_d, nq, cand_scores_d, cand_rows_d, (uint8_t*)ws_d, (hipStream_t)stream, row_mask_d);
 }
 
 int rfx_topk_merge(const float* cand_scores_d, const void* cand_rows_d, int rows_are_i64, int64_t nq, int64_t n_cand,
@@ -597,6 +609,12 @@ int rfx_dbg_stream_read(rfx_index_t h, void* scratch4_d, void* stream) {
 
 int rfx_search(rfx_index_t h, const void* queries_d, int64_t nq, int k, float* out_scores_d, int64_t* out_rows_d,
                void* ws_d, size_t ws_bytes, void* stream) {
+  return rfx_search_masked(h, queries_d, nq, k, nullptr, 0, out_scores_d, out_rows_d, ws_d, ws_bytes, stream);
+}
+
+int rfx_search_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d,
+                      int64_t mask_words, float* out_scores_d, int64_t* out_rows_d, void* ws_d, size_t ws_bytes,
+                      void* stream) {
   auto ix = get(h);
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
   std::shared_lock<std::shared_mutex> lk(ix->mu);
@@ -605,12 +623,15 @@ int rfx_search(rfx_index_t h, const void* queries_d, int64_t nq, int k, float* o
   if (rc) return rc;
   if (ws_bytes < L.total || (L.total && !ws_d)) return fail(RFX_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, L.total);
   if (nq > 0 && (!queries_d || !out_scores_d || !out_rows_d)) return fail(RFX_EINVAL, "null queries / outputs");
+  if (row_mask_d && mask_words < (ix->rows + 31) / 32)
+    return fail(RFX_EINVAL, "row mask has %lld words, the index needs %lld", (long long)mask_words,
+                (long long)((ix->rows + 31) / 32));
   RFX_HIP(hipSetDevice(ix->device));
   hipStream_t st = (hipStream_t)stream;
   uint8_t* ws = (uint8_t*)ws_d;
   float* cs = (float*)(ws + L.cs_off);
   int32_t* cr = (int32_t*)(ws + L.cr_off);
-  rc = scan_into(*ix, L, queries_d, nq, cs, cr, ws, st);
+  rc = scan_into(*ix, L, queries_d, nq, cs, cr, ws, st, row_mask_d);
   if (rc) return rc;
   // one pass over all candidates: the list-heads prefilter (list_len > 1) measured slower on the
   // scan's output (14 vs 19 us at 256 x 5120 candidates, tools/merge_bench.py)

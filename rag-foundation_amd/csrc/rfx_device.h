@@ -18,6 +18,25 @@ __device__ __forceinline__ bool better64(float s1, long long r1, float s2, long 
   return s1 > s2 || (s1 == s2 && r1 < r2);
 }
 
+// ---- row masks (metadata filters): bit (r & 31) of word r >> 5 set = row r may be returned ------
+// A lane of a 32x32 MFMA accumulator holds rows rb + (r & 3) + 8 (r >> 2), r < 16, with
+// rb ≡ 0 or 4 (mod 32): all in word rb >> 5.  acc_row_bits puts row (r & 3) + 8 (r >> 2) of the
+// lane at that bit; words past the mask (rows past the end, NaN anyway) read as 0.
+__device__ __forceinline__ uint32_t acc_row_bits(const uint32_t* __restrict__ mask, int rb, int nrows) {
+  const int w = rb >> 5;
+  return w < ((nrows + 31) >> 5) ? mask[w] >> (rb & 31) : 0u;
+}
+// masked-out rows become NaN, which no top-k compare admits (the tombstone rule)
+template <class V>
+__device__ __forceinline__ void mask_acc16(V& acc, uint32_t bits) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    if (!((bits >> ((r & 3) + 8 * (r >> 2))) & 1u)) acc[r] = __builtin_nanf("");
+}
+__device__ __forceinline__ bool row_allowed(const uint32_t* __restrict__ mask, int row) {
+  return (mask[row >> 5] >> (row & 31)) & 1u;
+}
+
 // ---- counter-based generator (oracle/synth.py restates this bit-for-bit) ----------------
 __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;

@@ -23,8 +23,10 @@ struct ValuPlan {
 };
 int valu_k_slot(int k);
 ValuPlan plan_scan_valu(int64_t nrows, int D, int dtype, int64_t nq, int k);
+// mask (every scan launcher): optional row mask, bit (r & 31) of word r >> 5 set = row r may be
+// returned, (nrows + 31) / 32 words; nullptr = all rows (the production kernels run unchanged).
 int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dtype, const float* Qf,
-                     int nq, float* cs, int* cr, hipStream_t st);
+                     int nq, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
 
 // ---- MFMA scan (batched bf16 / f16) -------------------------------------------------------
 struct MfmaPlan {
@@ -40,17 +42,17 @@ struct MfmaPlan {
 };
 MfmaPlan plan_scan_mfma(int64_t nrows, int D, int dtype, int64_t nq, int k);
 int launch_scan_mfma(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad,
-                     int nq, float* cs, int* cr, hipStream_t st);
+                     int nq, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
 int launch_scan_mfma_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, int D, const void* Qpad, int nq,
                          float* cs, int* cr, hipStream_t st);
 MfmaPlan plan_scan_mfma2(int64_t nrows, int D, int dtype, int64_t nq, int k);
 int launch_scan_mfma2(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st);
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
 int launch_scan_mfma2_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, int D, const void* Qpad, int nq,
                           uint32_t* tau, float* cs, int* cr, hipStream_t st);
 MfmaPlan plan_scan_mfma3(int64_t nrows, int D, int dtype, int64_t nq, int k);
 int launch_scan_mfma3(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st);
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
 size_t tau_bytes_mfma4(const MfmaPlan& p);
 MfmaPlan plan_scan_mfma4(int64_t nrows, int D, int dtype, int64_t nq, int k);
 int launch_scan_mfma4(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
@@ -60,7 +62,7 @@ int launch_scan_mfma4_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
 size_t tau_bytes_mfma5(const MfmaPlan& p);
 MfmaPlan plan_scan_mfma5(int64_t nrows, int D, int dtype, int64_t nq, int k);
 int launch_scan_mfma5(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st);
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
 int launch_scan_mfma5_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, int dtype, const void* Qpad, int nq,
                           uint32_t* tau, float* cs, int* cr, hipStream_t st);
 void launch_pad_queries(const void* Q, int64_t nq, int64_t nq_pad, int D, int esz, void* out,

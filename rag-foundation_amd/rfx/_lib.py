@@ -79,6 +79,8 @@ SIGNATURES = {
     "rfx_search": ([_u64, _p, _i64, _i, _p, _p, _p, _sz, _p], _i),
     "rfx_scan_plan": ([_u64, _i64, _i, _pi, _pi64], _i),
     "rfx_scan_topk": ([_u64, _p, _i64, _i, _p, _p, _p, _sz, _p], _i),
+    "rfx_search_masked": ([_u64, _p, _i64, _i, _p, _i64, _p, _p, _p, _sz, _p], _i),
+    "rfx_scan_topk_masked": ([_u64, _p, _i64, _i, _p, _i64, _p, _p, _p, _sz, _p], _i),
     "rfx_topk_merge": ([_p, _p, _i, _i64, _i64, _i, _i64, _p, _p, _p], _i),
     "rfx_scan_list_len": ([_u64, _i64, _i, _p], _i),
     "rfx_topk_merge_lists": ([_p, _p, _i, _i64, _i64, _i, _i, _i64, _p, _p, _p], _i),

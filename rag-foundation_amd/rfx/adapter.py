@@ -7,8 +7,9 @@ Mirrors the duck-typed surface of the reference adapter
   upload_file(store, path, *, display_name, custom_metadata, chunking_config) -> UploadResult
                                                                   ingestion.py:52
   op_status(op) -> {name, done, metadata, error}                  ingestion.py:119, uploads.py:335
-  ask_stream(*, contents, store_names, metadata_filter, model, system) -> 2 chunks
+  ask_stream(*, contents, store_names, metadata_filter, model, system, top_k=None) -> 2 chunks
                                                                   chat.py:499-505
+    (metadata_filter -> row mask, rfx.filters; top_k: the request's k, §8f item 3)
   ask(...) -> response                                            (interface completeness)
   extract_citations_from_response(resp) -> [citation dicts]       chat.py:578
   new_stream_ids() -> (uuid4, uuid4)                              chat.py:979
@@ -92,6 +93,9 @@ class LocalGpuRag:
             retriever = GpuRetriever()
         self.retriever = retriever
         self.top_k = int(os.environ.get("RFX_TOP_K", "5")) if top_k is None else int(top_k)
+        # metadata filters become row masks; RFX_METADATA_FILTER=0 ignores them
+        # like the reference mock (gemini_rag.py:673-694)
+        self.apply_filters = os.environ.get("RFX_METADATA_FILTER", "1") != "0"
         self.is_mock = True
 
     # -------- Stores --------
@@ -134,19 +138,27 @@ class LocalGpuRag:
         self.retriever.delete_file(store_name, file_id)
 
     # -------- Query (sync & stream) --------
-    def retrieve(self, question: str, store_names: Sequence[str], k: Optional[int] = None):
-        return self.retriever.search(list(store_names or []), question, self.top_k if k is None else int(k))
+    def retrieve(self, question: str, store_names: Sequence[str], k: Optional[int] = None,
+                 metadata_filter: Optional[Any] = None):
+        """Top-k hits.  k: the request's top_k (the reference route drops it,
+        chat.py:66), default self.top_k; 1..64."""
+        filt = metadata_filter if self.apply_filters else None
+        return self.retriever.search(list(store_names or []), question, self.top_k if k is None else int(k),
+                                     metadata_filter=filt)
 
     def ask(self, *, contents: Any, store_names: Sequence[str], metadata_filter: Optional[Any], model: str,
-            system: Optional[str] = None) -> Any:
+            system: Optional[str] = None, top_k: Optional[int] = None) -> Any:
         with observe("generate"):
-            return build_response(self.retrieve(contents_to_text(contents), store_names), store_names)
+            hits = self.retrieve(contents_to_text(contents), store_names, top_k, metadata_filter)
+            return build_response(hits, store_names)
 
     def ask_stream(self, *, contents: Any, store_names: Sequence[str], metadata_filter: Optional[Any], model: str,
-                   system: Optional[str] = None):
+                   system: Optional[str] = None, top_k: Optional[int] = None):
+        """The reference's keyword set plus an optional top_k (callers that do not pass it get
+        self.top_k, so the reference call site chat.py:499-505 works unchanged)."""
         with observe("generate_stream"):
             text = contents_to_text(contents)
-            resp = build_response(self.retrieve(text, store_names), store_names)
+            resp = build_response(self.retrieve(text, store_names, top_k, metadata_filter), store_names)
         yield SimpleNamespace(text=f"[mock-mode] {text or 'response'}", candidates=None,
                               usage_metadata=SimpleNamespace(prompt_token_count=0, candidates_token_count=0))
         yield resp

@@ -121,8 +121,23 @@ class DeviceIndex:
             raise ValueError(f"queries must be a cuda {self.torch_dtype} tensor [nq][{self.dim}]")
         return q.contiguous()
 
-    def search(self, queries: torch.Tensor, k: int, workspace: torch.Tensor = None, stream=None):
-        """Top-k rows per query: (scores f32 [nq][k], rows int64 [nq][k]) on the device."""
+    def _check_mask(self, row_mask, dev):
+        """row_mask: None, or a device int32/uint32 bitmap (bit r & 31 of word r >> 5 = row r allowed)
+        of at least (rows + 31) // 32 words (make_row_mask)."""
+        if row_mask is None:
+            return None, 0
+        if row_mask.dtype not in (torch.int32, torch.uint32) or row_mask.dim() != 1 or not row_mask.is_contiguous():
+            raise ValueError("row mask must be a contiguous 1-D int32/uint32 tensor")
+        if row_mask.device != dev:
+            raise ValueError(f"row mask on {row_mask.device}, queries on {dev}")
+        if row_mask.numel() < (self.rows + 31) // 32:
+            raise ValueError(f"row mask has {row_mask.numel()} words, index needs {(self.rows + 31) // 32}")
+        return row_mask, row_mask.numel()
+
+    def search(self, queries: torch.Tensor, k: int, workspace: torch.Tensor = None, stream=None,
+               row_mask: torch.Tensor = None):
+        """Top-k rows per query: (scores f32 [nq][k], rows int64 [nq][k]) on the device.
+        row_mask (optional): only rows whose bit is set are returned (metadata filter)."""
         q = self._check_queries(queries)
         nq = q.shape[0]
         dev = q.device
@@ -131,9 +146,14 @@ class DeviceIndex:
         need = self.workspace_bytes(nq, k)
         ws = workspace if workspace is not None and workspace.numel() >= need else \
             torch.empty(max(need, 1), dtype=torch.uint8, device=dev)
+        m, mw = self._check_mask(row_mask, dev)
         with torch.cuda.device(dev):
-            check(lib.rfx_search(self.handle, ptr(q), nq, int(k), ptr(out_s), ptr(out_r), ptr(ws), ws.numel(),
-                                 stream_ptr(stream)))
+            if m is None:
+                check(lib.rfx_search(self.handle, ptr(q), nq, int(k), ptr(out_s), ptr(out_r), ptr(ws), ws.numel(),
+                                     stream_ptr(stream)))
+            else:
+                check(lib.rfx_search_masked(self.handle, ptr(q), nq, int(k), ptr(m), mw, ptr(out_s), ptr(out_r),
+                                            ptr(ws), ws.numel(), stream_ptr(stream)))
         return out_s, out_r
 
     def list_len(self, nq: int, k: int) -> int:
@@ -147,7 +167,8 @@ class DeviceIndex:
         check(lib.rfx_scan_plan(self.handle, int(nq), int(k), ctypes.byref(kern), ctypes.byref(ncand)))
         return kern.value, ncand.value
 
-    def scan(self, queries: torch.Tensor, k: int, workspace: torch.Tensor = None, stream=None):
+    def scan(self, queries: torch.Tensor, k: int, workspace: torch.Tensor = None, stream=None,
+             row_mask: torch.Tensor = None):
         """Fused scan only: per-query candidate lists (scores f32 [nq][n_cand], local rows int32)."""
         q = self._check_queries(queries)
         nq = q.shape[0]
@@ -157,9 +178,14 @@ class DeviceIndex:
         need = self.workspace_bytes(nq, k)
         ws = workspace if workspace is not None and workspace.numel() >= need else \
             torch.empty(max(need, 1), dtype=torch.uint8, device=q.device)
+        m, mw = self._check_mask(row_mask, q.device)
         with torch.cuda.device(q.device):
-            check(lib.rfx_scan_topk(self.handle, ptr(q), nq, int(k), ptr(cs), ptr(cr), ptr(ws), ws.numel(),
-                                    stream_ptr(stream)))
+            if m is None:
+                check(lib.rfx_scan_topk(self.handle, ptr(q), nq, int(k), ptr(cs), ptr(cr), ptr(ws), ws.numel(),
+                                        stream_ptr(stream)))
+            else:
+                check(lib.rfx_scan_topk_masked(self.handle, ptr(q), nq, int(k), ptr(m), mw, ptr(cs), ptr(cr),
+                                               ptr(ws), ws.numel(), stream_ptr(stream)))
         return cs, cr
 
 

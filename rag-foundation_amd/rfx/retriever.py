@@ -8,6 +8,7 @@ from dataclasses import dataclass
 
 import torch
 
+from . import filters
 from .batcher import GroupBatcher
 from .embedder import DEFAULT_MAX_TOKENS, DEFAULT_OVERLAP, Embedder
 from .store import registry as default_registry
@@ -92,40 +93,57 @@ class GpuRetriever:
         return bool(st and st.delete_file(file_id))
 
     # ---- retrieval ----------------------------------------------------------------------------
-    def _search_store_batch(self, st, items):
+    def _search_store_batch(self, st, items, row_mask=None):
         """One GPU search for a batch of (question, k) against one store: one embedding GEMM,
         one scan + merge at the largest k; each item gets its own first k."""
         kmax = max(k for _, k in items)
         with torch.cuda.device(st.device):
             q = self.embedder(st.dim).embed_texts([t for t, _ in items], st.dtype)
-            s, r = st.index.search(q, kmax)
+            s, r = st.index.search(q, kmax, row_mask=row_mask)
             s, r = s.cpu().tolist(), r.cpu().tolist()
         return [(s[i][:k], r[i][:k]) for i, (_, k) in enumerate(items)]
 
-    def _batcher(self, st):
-        key = (st.name, id(st))
+    def _batcher(self, st, fkey, row_mask):
+        # one batcher per (store, filter): a launch applies one row mask to all its queries
+        key = (st.name, id(st), fkey, st.version)
         with _STATE_LOCK:
             b = _BATCHERS.get(key)
             if b is None:
-                b = GroupBatcher(lambda items, st=st: self._search_store_batch(st, items), max_batch=256)
+                b = GroupBatcher(lambda items, st=st, m=row_mask: self._search_store_batch(st, items, m),
+                                 max_batch=256)
+                for old in [k for k in _BATCHERS if k[:3] == key[:3]]:
+                    del _BATCHERS[old]  # an older version's mask
+                if len(_BATCHERS) >= 1024:
+                    _BATCHERS.clear()
                 _BATCHERS[key] = b
             return b
 
-    def search_store(self, st, question, k):
-        """(scores, rows) of one question against one store; batched with concurrent callers."""
+    def search_store(self, st, question, k, metadata_filter=None):
+        """(scores, rows) of one question against one store, or None when the filter selects no
+        row of it; batched with concurrent callers of the same store and filter."""
+        mask = st.row_mask(metadata_filter) if metadata_filter is not None else None
+        if metadata_filter is not None and mask is None:
+            return None
         if self.batching:
-            return self._batcher(st).submit((question, int(k)))
-        return self._search_store_batch(st, [(question, int(k))])[0]
+            return self._batcher(st, filters.filter_key(metadata_filter), mask).submit((question, int(k)))
+        return self._search_store_batch(st, [(question, int(k))], mask)[0]
 
-    def search(self, store_names, question, k):
+    def search(self, store_names, question, k, metadata_filter=None):
         """Top-k hits over the union of the named stores, rank order (score desc, store order,
-        row asc)."""
+        row asc).  metadata_filter: {key: scalar | [scalars]} over upload metadata (rfx.filters)."""
+        k = int(k)
+        if not 1 <= k <= 64:
+            raise ValueError(f"top_k={k} out of range [1, 64]")
+        filt = filters.check_filter(metadata_filter)
         hits = []
         for si, name in enumerate(store_names or []):
             st = self.registry.get(name)
             if st is None or st.index.rows == 0:
                 continue
-            s, r = self.search_store(st, question, k)
+            res = self.search_store(st, question, k, filt)
+            if res is None:
+                continue
+            s, r = res
             for sc, row in zip(s, r):
                 if row < 0:
                     continue

@@ -15,6 +15,9 @@ import shutil
 import threading
 import uuid
 
+import torch
+
+from . import filters
 from .index import DeviceIndex
 
 STORE_PREFIX = "fileSearchStores/"  # accepted by routes/stores.py:46 (prefix check)
@@ -34,6 +37,7 @@ class LocalStore:
         self.version = 0
         self.lock = threading.RLock()
         self._mtime = None
+        self._masks = {}    # (version, filter key) -> device row mask
 
     # ---- persistence ------------------------------------------------------------------------
     def _manifest(self):
@@ -64,6 +68,7 @@ class LocalStore:
         st.version = man["version"]
         st.files = man["files"]
         st.lock = threading.RLock()
+        st._masks = {}
         idx = os.path.join(path, "index.rfx")
         st.index = DeviceIndex.load(idx, device) if os.path.exists(idx) else DeviceIndex(st.dim, st.dtype, device)
         st.rows = []
@@ -107,6 +112,25 @@ class LocalStore:
             self.version += 1
             self.save()
             return True
+
+    def row_mask(self, metadata_filter):
+        """Device row mask (int32 words) of the live files whose upload metadata matches the
+        filter (rfx.filters), or None when no file matches.  Cached per (store version, filter)."""
+        key = (self.version, filters.filter_key(metadata_filter))
+        with self.lock:
+            if key in self._masks:
+                return self._masks[key]
+            ranges = [(f["first"], f["n"]) for f in self.files.values()
+                      if not f["deleted"] and f["n"] and
+                      filters.file_matches(filters.normalize_metadata(f.get("metadata")), metadata_filter)]
+            mask = None
+            if ranges:
+                words = filters.row_mask_words(self.index.rows, ranges)
+                mask = torch.from_numpy(words).to(f"cuda:{self.device}")
+            if len(self._masks) >= 64:
+                self._masks.clear()
+            self._masks[key] = mask
+            return mask
 
     def row_info(self, row):
         fid, text = self.rows[row]

@@ -8,6 +8,7 @@ from oracle import embed as oembed
 from oracle import search as osearch
 from oracle import synth as osynth
 from oracle import textproc
+from rfx import filters
 from rfx.retriever import Hit, _chunking
 
 V, DIM = 4096, 768
@@ -49,7 +50,7 @@ class OracleRetriever:
         first = len(st["rows"])
         st["rows"] += [(fid, c) for c in chunks]
         st["vecs"] = np.concatenate([st["vecs"], self._embed(chunks)]) if chunks else st["vecs"]
-        st["files"][fid] = {"first": first, "n": len(chunks), "title": display_name}
+        st["files"][fid] = {"first": first, "n": len(chunks), "title": display_name, "metadata": metadata}
         return fid, len(chunks)
 
     def delete_file(self, store_name, file_id):
@@ -60,14 +61,24 @@ class OracleRetriever:
         st["vecs"][f["first"]:f["first"] + f["n"]] = np.nan
         return True
 
-    def search(self, store_names, question, k):
+    def search(self, store_names, question, k, metadata_filter=None):
+        if not 1 <= int(k) <= 64:
+            raise ValueError(f"top_k={k} out of range [1, 64]")
+        filt = filters.check_filter(metadata_filter)
         hits = []
         q = self._embed([question])
         for si, name in enumerate(store_names or []):
             st = self.stores.get(name)
             if not st or not st["rows"]:
                 continue
-            s, r = osearch.topk(q, st["vecs"], k)
+            vecs = st["vecs"]
+            if filt is not None:  # rows of non-matching files are excluded (NaN, the tombstone rule)
+                keep = np.zeros(len(vecs), dtype=bool)
+                for f in st["files"].values():
+                    if filters.file_matches(filters.normalize_metadata(f["metadata"]), filt):
+                        keep[f["first"]:f["first"] + f["n"]] = True
+                vecs = np.where(keep[:, None], vecs, np.nan)
+            s, r = osearch.topk(q, vecs, k)
             for sc, row in zip(s[0], r[0]):
                 if row < 0:
                     continue

@@ -87,11 +87,62 @@ def test_citation_frames_wire_format(rag, store_with_doc):
         assert payload["title"] == "sample-report.md" and payload["snippet"]
 
 
-def test_metadata_filter_accepted(rag, store_with_doc):
+def test_metadata_filter_ignored_when_disabled(rag, store_with_doc):
+    # RFX_METADATA_FILTER=0: the reference mock's behaviour (filter accepted and ignored)
     st, _ = store_with_doc
+    rag.apply_filters = False
     a = rag.ask(contents="demo", store_names=[st], metadata_filter={"tenant": "acme", "region": ["a", "b"]}, model="m")
     b = rag.ask(contents="demo", store_names=[st], metadata_filter=None, model="m")
     assert rag.extract_citations_from_response(a) == rag.extract_citations_from_response(b)
+
+
+def _two_tenant_store(rag, tmp_path):
+    st = rag.create_store("tenants")
+    ids = {}
+    for tenant, words in (("acme", "alpha beta gamma delta " * 8), ("globex", "alpha beta epsilon zeta " * 8)):
+        p = tmp_path / f"{tenant}.txt"
+        p.write_text(words)
+        up = rag.upload_file(st, str(p), display_name=f"{tenant}.txt",
+                             custom_metadata=[{"key": "tenant", "string_value": tenant},
+                                              {"key": "year", "numeric_value": 2024 if tenant == "acme" else 2025}],
+                             chunking_config={"white_space_config": {"max_tokens_per_chunk": 4, "max_overlap_tokens": 0}})
+        ids[tenant] = up.file_id
+    return st, ids
+
+
+def test_metadata_filter_selects_files(rag, tmp_path):
+    st, ids = _two_tenant_store(rag, tmp_path)
+
+    def titles(filt, k=20):
+        r = rag.ask(contents="alpha beta", store_names=[st], metadata_filter=filt, model="m", top_k=k)
+        return [c["title"] for c in rag.extract_citations_from_response(r)]
+
+    everything = titles(None)
+    assert set(everything) == {"acme.txt", "globex.txt"}
+    assert titles({"tenant": "acme"}) == [t for t in everything if t == "acme.txt"]
+    assert titles({"tenant": ["acme", "globex"]}) == everything
+    assert titles({"year": 2025}) == [t for t in everything if t == "globex.txt"]
+    assert titles({"year": 2025.0, "tenant": "globex"}) == [t for t in everything if t == "globex.txt"]
+    assert titles({"tenant": "acme", "year": 2025}) == []  # AND over keys
+    assert titles({"tenant": "initech"}) == []
+    assert titles({"missing_key": "x"}) == []
+    with pytest.raises(ValueError):
+        titles("tenant=acme")
+    with pytest.raises(ValueError):
+        titles({"tenant": []})
+
+
+def test_top_k_end_to_end(rag, tmp_path):
+    st, _ = _two_tenant_store(rag, tmp_path)
+    q = [{"role": "user", "parts": [{"text": "alpha beta"}]}]
+    for k in (1, 3, 7, 16):
+        chunks = list(rag.ask_stream(contents=q, store_names=[st], metadata_filter=None, model="m", top_k=k))
+        assert len(chunks[1].candidates[0].grounding_metadata.grounding_chunks) == k
+    default = list(rag.ask_stream(contents=q, store_names=[st], metadata_filter=None, model="m"))
+    assert len(default[1].candidates[0].grounding_metadata.grounding_chunks) == rag.top_k
+    for bad in (0, 65):
+        with pytest.raises(ValueError):
+            list(rag.ask_stream(contents=q, store_names=[st], metadata_filter=None, model="m", top_k=bad))
 
 
 def test_empty_and_unknown_stores(rag):
