@@ -175,6 +175,43 @@ int rfx_embed(const int32_t* indptr_d, const int32_t* bucket_d, const int16_t* c
 /* ---- synthetic rows (tests / bench) --------------------------------------------------------- */
 int rfx_synth_rows(uint64_t seed, int64_t row0, int64_t n, int dim, int dtype, void* out_d,
                    void* stream);
+/* Clustered rows (IVF tests / config 5): normalise(centre(cluster(r)) + noise(r)); centres from
+ * cseed (shared by corpus and queries), cluster(r) and noise from seed (oracle/ivf.py). */
+int rfx_synth_clustered(uint64_t cseed, int64_t ncenters, uint64_t seed, int64_t row0, int64_t n,
+                        int dim, int dtype, void* out_d, void* stream);
+
+/* ---- IVF-Flat int8 (build plan item 8) -------------------------------------
+ * No reference counterpart: the reference's only large-corpus answer is Gemini's managed index
+ * (gemini_rag.py:463-469).  This extends the brute-force path for corpora where scanning every
+ * row per batch is not wanted: a k-means coarse quantiser (int8 centroids, MFMA i8 scoring),
+ * int8 posting lists, and a posting-list scan (v_dot4 against LDS-staged queries).  Numerics are
+ * exact integer/IEEE steps restated by oracle/ivf.py (bit-exact); recall vs brute force < 1 by
+ * design.  dim in {256, 512, 768, 1024}; nlist <= 16384; nprobe, k <= 64.
+ * Lifecycle: create -> train (or set_centroids, e.g. broadcast from rank 0) -> add (quantise +
+ * assign; posting lists rebuilt lazily) -> search. */
+typedef uint64_t rfx_ivf_t;
+int rfx_ivf_create(int device, int dim, int nlist, rfx_ivf_t* out);
+int rfx_ivf_destroy(rfx_ivf_t h);
+int rfx_ivf_info(rfx_ivf_t h, int* dim, int* nlist, int64_t* rows, int* trained);
+/* k-means over n >= nlist sample rows (device, dtype f32/bf16/f16), iters Lloyd iterations */
+int rfx_ivf_train(rfx_ivf_t h, const void* rows_d, int64_t n, int dtype, int iters, void* stream);
+int rfx_ivf_set_centroids(rfx_ivf_t h, const int8_t* centroids_d /* [nlist][dim] */, void* stream);
+int rfx_ivf_get_centroids(rfx_ivf_t h, int8_t* centroids_d, float* factors_d, void* stream);
+int rfx_ivf_add(rfx_ivf_t h, const void* rows_d, int64_t n, int dtype, void* stream);
+int rfx_ivf_build(rfx_ivf_t h, void* stream);
+/* inspection (tests): per-row codes / scales / list labels in insertion order; list offsets
+ * [nlist+1] and row ids in list order */
+int rfx_ivf_codes(rfx_ivf_t h, int8_t* codes_d, float* inv_d, int32_t* labels_d, void* stream);
+int rfx_ivf_lists(rfx_ivf_t h, int64_t* offsets_d, int32_t* ids_d, void* stream);
+int rfx_ivf_search_workspace_bytes(rfx_ivf_t h, int64_t nq, int k, int nprobe, size_t* out_bytes);
+/* queries_d [nq][dim] (dtype); outputs [nq][k] scores f32 / rows i64 (insertion-order row ids),
+ * padded (-inf, -1) */
+int rfx_ivf_search(rfx_ivf_t h, const void* queries_d, int64_t nq, int dtype, int k, int nprobe,
+                   float* out_scores_d, int64_t* out_rows_d, void* ws_d, size_t ws_bytes,
+                   void* stream);
+/* int8 quantisation of rows (the IVF code format): codes [n][dim], inv [n] = amax / 127 */
+int rfx_quantize(const void* rows_d, int64_t n, int dim, int dtype, int8_t* codes_d, float* inv_d,
+                 void* stream);
 
 #ifdef __cplusplus
 }

@@ -19,10 +19,6 @@ namespace rfx {
 // normalised exactly (int64 sum of squares, f64 sqrt/div) then rounded to f32 then dtype.
 // oracle/synth.py is the CPU restatement (bit-identical).
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ int32_t synth_raw(uint64_t base, uint64_t idx) {
-  const uint64_t u = splitmix64(base + idx);
-  return (int32_t)(2u * (uint32_t)(u >> 40)) + 1 - (1 << 24);
-}
 
 template <int DT>
 __global__ __launch_bounds__(256) void synth_rows_kernel(uint64_t base, int64_t row0, int64_t n,

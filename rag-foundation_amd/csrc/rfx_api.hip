@@ -192,6 +192,18 @@ int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq,
 
 }  // namespace
 
+namespace rfx {
+int api_fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+}  // namespace rfx
+
 extern "C" {
 
 const char* rfx_last_error(void) { return g_err.c_str(); }

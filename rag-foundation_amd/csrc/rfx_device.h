@@ -45,6 +45,12 @@ __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
+// odd integer in (-2^24, 2^24) of generator key idx (oracle/synth.py raw_rows)
+__device__ __forceinline__ int32_t synth_raw(uint64_t base, uint64_t idx) {
+  const uint64_t u = splitmix64(base + idx);
+  return (int32_t)(2u * (uint32_t)(u >> 40)) + 1 - (1 << 24);
+}
+
 // ---- fp32 <-> 16-bit storage -----------------------------------------------------------------
 __device__ __forceinline__ float bf16_to_f32(uint16_t h) {
   return __uint_as_float(((uint32_t)h) << 16);

@@ -82,4 +82,32 @@ void launch_embed_weights(int V, int dim, uint64_t seed, void* wt, hipStream_t s
 int launch_embed(const int32_t* indptr, const int32_t* bucket, const int16_t* count, int64_t n, int V,
                  const void* wt, int dim, void* out, int out_dtype, void* ws, hipStream_t st);
 
+// ---- IVF-Flat int8 (k_ivf.hip) --------------------------------------------------------------------
+namespace ivf {
+void launch_synth_clustered(uint64_t cseed, uint64_t ncenters, uint64_t seed, int64_t row0, int64_t n, int dim,
+                            int dtype, void* out, hipStream_t st);
+void launch_quantize(const void* X, int64_t n, int dim, int dtype, int8_t* codes, float* inv, hipStream_t st);
+int launch_coarse_scores(const int8_t* X, int64_t n, const int8_t* C, int m, int D, const float* fc, float* S,
+                         int* ids, hipStream_t st);
+int launch_assign(const int8_t* X, int64_t n, const int8_t* C, int m, int D, const float* fc, int* labels,
+                  float* best, hipStream_t st);
+void launch_kmeans_accum(const int8_t* X, int64_t n, int D, const int* labels, int* sums, int* counts,
+                         hipStream_t st);
+// sums == nullptr: only recompute the factors of qc
+void launch_centroid_update(const int* sums, const int* counts, int m, int D, int8_t* qc, float* fc, hipStream_t st);
+size_t sort_temp_bytes(int64_t n);
+int launch_build_lists(const int* labels, int64_t n, int m, const int8_t* codes, const float* inv, int D,
+                       unsigned* keys_tmp, int* vals_tmp, unsigned* keys_out, int* ids_out, void* sort_tmp,
+                       size_t sort_tmp_bytes, int* counts, int64_t* off, int8_t* dcodes, float* dinv,
+                       hipStream_t st);
+int list_k(int k);
+int launch_group_pairs(const int64_t* probes, int P, int m, int* pair_off, int* pairs, hipStream_t st);
+int launch_list_scan(int K, int D, int m, const int8_t* codes, const float* inv, const int* ids, const int64_t* off,
+                     const int* pair_off, const int* pairs, int nprobe, const int8_t* qq, const float* qinv,
+                     float* cs, int* cr, hipStream_t st);
+}  // namespace ivf
+
+// error reporting shared by the C-ABI translation units (rfx_api.hip owns rfx_last_error)
+int api_fail(int code, const char* fmt, ...);
+
 }  // namespace rfx

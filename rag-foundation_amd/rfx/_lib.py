@@ -79,6 +79,20 @@ SIGNATURES = {
     "rfx_search": ([_u64, _p, _i64, _i, _p, _p, _p, _sz, _p], _i),
     "rfx_scan_plan": ([_u64, _i64, _i, _pi, _pi64], _i),
     "rfx_scan_topk": ([_u64, _p, _i64, _i, _p, _p, _p, _sz, _p], _i),
+    "rfx_synth_clustered": ([_u64, _i64, _u64, _i64, _i64, _i, _i, _p, _p], _i),
+    "rfx_quantize": ([_p, _i64, _i, _i, _p, _p, _p], _i),
+    "rfx_ivf_create": ([_i, _i, _i, _pu64], _i),
+    "rfx_ivf_destroy": ([_u64], _i),
+    "rfx_ivf_info": ([_u64, _pi, _pi, _pi64, _pi], _i),
+    "rfx_ivf_train": ([_u64, _p, _i64, _i, _i, _p], _i),
+    "rfx_ivf_set_centroids": ([_u64, _p, _p], _i),
+    "rfx_ivf_get_centroids": ([_u64, _p, _p, _p], _i),
+    "rfx_ivf_add": ([_u64, _p, _i64, _i, _p], _i),
+    "rfx_ivf_build": ([_u64, _p], _i),
+    "rfx_ivf_codes": ([_u64, _p, _p, _p, _p], _i),
+    "rfx_ivf_lists": ([_u64, _p, _p, _p], _i),
+    "rfx_ivf_search_workspace_bytes": ([_u64, _i64, _i, _i, _psz], _i),
+    "rfx_ivf_search": ([_u64, _p, _i64, _i, _i, _i, _p, _p, _p, _sz, _p], _i),
     "rfx_search_masked": ([_u64, _p, _i64, _i, _p, _i64, _p, _p, _p, _sz, _p], _i),
     "rfx_scan_topk_masked": ([_u64, _p, _i64, _i, _p, _i64, _p, _p, _p, _sz, _p], _i),
     "rfx_topk_merge": ([_p, _p, _i, _i64, _i64, _i, _i64, _p, _p, _p], _i),

@@ -1,0 +1,152 @@
+"""IvfIndex — IVF-Flat int8 index on one device (C ABI rfx_ivf_*, include/rfx.h; kernels
+csrc/k_ivf.hip).  SURVEY.md §8 config 5 / build plan item 8: a k-means coarse quantiser, int8
+posting lists, a posting-list scan; recall vs brute force < 1 by design.  Every call goes to the
+HIP library; there is no CPU path.
+
+Row-sharded multi-GPU use (rfx.dist): train on rank 0, broadcast `centroids()` and call
+`set_centroids` on the other ranks, add each rank's rows, then search per rank and merge the
+per-rank top-k exactly like the brute-force path (topk_merge_records / gather_merge_records).
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr, stream_ptr
+
+
+class IvfIndex:
+    def __init__(self, dim: int, nlist: int, device: int = 0):
+        self.dim, self.nlist, self.device = int(dim), int(nlist), int(device)
+        h = ctypes.c_uint64()
+        with torch.cuda.device(self.device):
+            check(lib.rfx_ivf_create(self.device, self.dim, self.nlist, ctypes.byref(h)))
+        self.handle = h.value
+
+    def close(self) -> None:
+        if getattr(self, "handle", None):
+            check(lib.rfx_ivf_destroy(self.handle))
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _dev(self):
+        return torch.device("cuda", self.device)
+
+    def _rows(self, rows: torch.Tensor):
+        if rows.dim() != 2 or rows.shape[1] != self.dim:
+            raise ValueError(f"rows must be [n][{self.dim}]")
+        dt = {v: k for k, v in _lib.TORCH_DTYPES.items()}.get(rows.dtype)
+        if dt is None:
+            raise ValueError("rows must be float32, bfloat16 or float16")
+        if rows.device != self._dev():
+            raise ValueError(f"rows on {rows.device}, index on {self._dev()}")
+        return rows.contiguous(), _lib.DTYPE_CODES[dt]
+
+    @property
+    def rows(self) -> int:
+        n = ctypes.c_int64()
+        check(lib.rfx_ivf_info(self.handle, None, None, ctypes.byref(n), None))
+        return n.value
+
+    @property
+    def trained(self) -> bool:
+        t = ctypes.c_int()
+        check(lib.rfx_ivf_info(self.handle, None, None, None, ctypes.byref(t)))
+        return bool(t.value)
+
+    def train(self, rows: torch.Tensor, iters: int = 10, stream=None) -> None:
+        """k-means over sample rows (>= nlist of them)."""
+        r, dt = self._rows(rows)
+        with torch.cuda.device(self.device):
+            check(lib.rfx_ivf_train(self.handle, ptr(r), r.shape[0], dt, int(iters), stream_ptr(stream)))
+
+    def centroids(self, stream=None):
+        """(int8 [nlist][dim], factors f32 [nlist]) on the device."""
+        qc = torch.empty((self.nlist, self.dim), dtype=torch.int8, device=self._dev())
+        fc = torch.empty((self.nlist,), dtype=torch.float32, device=self._dev())
+        with torch.cuda.device(self.device):
+            check(lib.rfx_ivf_get_centroids(self.handle, ptr(qc), ptr(fc), stream_ptr(stream)))
+        return qc, fc
+
+    def set_centroids(self, qc: torch.Tensor, stream=None) -> None:
+        if qc.dtype != torch.int8 or tuple(qc.shape) != (self.nlist, self.dim) or qc.device != self._dev():
+            raise ValueError(f"centroids must be int8 [{self.nlist}][{self.dim}] on {self._dev()}")
+        qc = qc.contiguous()
+        with torch.cuda.device(self.device):
+            check(lib.rfx_ivf_set_centroids(self.handle, ptr(qc), stream_ptr(stream)))
+
+    def add(self, rows: torch.Tensor, stream=None) -> int:
+        """Quantise + assign rows; returns the first row id."""
+        r, dt = self._rows(rows)
+        first = self.rows
+        with torch.cuda.device(self.device):
+            check(lib.rfx_ivf_add(self.handle, ptr(r), r.shape[0], dt, stream_ptr(stream)))
+        return first
+
+    def build(self, stream=None) -> None:
+        with torch.cuda.device(self.device):
+            check(lib.rfx_ivf_build(self.handle, stream_ptr(stream)))
+
+    def codes(self, stream=None):
+        """(codes int8 [rows][dim], inv f32 [rows], labels int32 [rows]) in insertion order."""
+        n = self.rows
+        c = torch.empty((n, self.dim), dtype=torch.int8, device=self._dev())
+        inv = torch.empty((n,), dtype=torch.float32, device=self._dev())
+        lab = torch.empty((n,), dtype=torch.int32, device=self._dev())
+        with torch.cuda.device(self.device):
+            check(lib.rfx_ivf_codes(self.handle, ptr(c), ptr(inv), ptr(lab), stream_ptr(stream)))
+        return c, inv, lab
+
+    def lists(self, stream=None):
+        """(offsets int64 [nlist+1], row ids int32 [rows] in list order)."""
+        off = torch.empty((self.nlist + 1,), dtype=torch.int64, device=self._dev())
+        ids = torch.empty((max(self.rows, 1),), dtype=torch.int32, device=self._dev())
+        with torch.cuda.device(self.device):
+            check(lib.rfx_ivf_lists(self.handle, ptr(off), ptr(ids), stream_ptr(stream)))
+        return off, ids[:self.rows]
+
+    def workspace_bytes(self, nq: int, k: int, nprobe: int) -> int:
+        b = ctypes.c_size_t()
+        check(lib.rfx_ivf_search_workspace_bytes(self.handle, int(nq), int(k), int(nprobe), ctypes.byref(b)))
+        return b.value
+
+    def search(self, queries: torch.Tensor, k: int, nprobe: int, workspace: torch.Tensor = None, stream=None):
+        """Top-k rows per query over the nprobe nearest lists: (scores f32 [nq][k], rows i64 [nq][k])."""
+        q, dt = self._rows(queries)
+        nq = q.shape[0]
+        out_s = torch.empty((nq, k), dtype=torch.float32, device=self._dev())
+        out_r = torch.empty((nq, k), dtype=torch.int64, device=self._dev())
+        need = self.workspace_bytes(nq, k, nprobe)
+        ws = workspace if workspace is not None and workspace.numel() >= need else \
+            torch.empty(max(need, 1), dtype=torch.uint8, device=self._dev())
+        with torch.cuda.device(self.device):
+            check(lib.rfx_ivf_search(self.handle, ptr(q), nq, dt, int(k), int(nprobe), ptr(out_s), ptr(out_r),
+                                     ptr(ws), ws.numel(), stream_ptr(stream)))
+        return out_s, out_r
+
+
+def quantize(rows: torch.Tensor, stream=None):
+    """int8 codes [n][dim] + inv scales [n] of rows (the IVF code format)."""
+    dt = {v: k for k, v in _lib.TORCH_DTYPES.items()}[rows.dtype]
+    rows = rows.contiguous()
+    n, d = rows.shape
+    codes = torch.empty((n, d), dtype=torch.int8, device=rows.device)
+    inv = torch.empty((n,), dtype=torch.float32, device=rows.device)
+    with torch.cuda.device(rows.device):
+        check(lib.rfx_quantize(ptr(rows), n, d, _lib.DTYPE_CODES[dt], ptr(codes), ptr(inv), stream_ptr(stream)))
+    return codes, inv
+
+
+def synth_clustered(cseed: int, ncenters: int, seed: int, row0: int, n: int, dim: int, dtype: str = "bf16",
+                    device: int = 0) -> torch.Tensor:
+    """Clustered synthetic rows on the device (oracle/ivf.py clustered_rows)."""
+    out = torch.empty((n, dim), dtype=_lib.TORCH_DTYPES[dtype], device=torch.device("cuda", device))
+    with torch.cuda.device(device):
+        check(lib.rfx_synth_clustered(ctypes.c_uint64(cseed), int(ncenters), ctypes.c_uint64(seed), int(row0), int(n),
+                                      int(dim), _lib.DTYPE_CODES[dtype], ptr(out), stream_ptr()))
+    return out

@@ -52,8 +52,11 @@ def test_hip_imports_resolve_in_torch_runtime():
 def test_lib_targets_gfx950_only():
     from rfx import _lib
     out = subprocess.run(["strings", _lib.LIB_PATH], capture_output=True, text=True).stdout
-    assert "gfx950" in out
-    assert "gfx942" not in out and "gfx90a" not in out
+    # every offload bundle (code object) targets gfx950; (rocPRIM's headers carry other arch names
+    # as data, so match the bundle target ids, not any mention)
+    import re
+    targets = set(re.findall(r"amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", out))
+    assert targets == {"gfx950"}, targets
 
 
 def test_version_and_error_string():
