@@ -248,11 +248,8 @@ int rfx_ivf_train(rfx_ivf_t h, const void* rows_d, int64_t n, int dtype, int ite
   int rc = RFX_OK;
   rfx::ivf::launch_quantize(rows_d, n, D, dtype, codes, inv, st);
   // initial centroids: sample rows j * (n / nlist)
-  const int64_t step = n / m;
-  for (int j = 0; j < m && rc == RFX_OK; ++j)
-    if (hipMemcpyAsync(iv->qc + (int64_t)j * D, codes + (int64_t)j * step * D, D, hipMemcpyDeviceToDevice, st) != hipSuccess)
-      rc = api_fail(RFX_EDEVICE, "centroid init copy failed");
-  if (rc == RFX_OK) rfx::ivf::launch_centroid_update(nullptr, nullptr, m, D, iv->qc, iv->fc, st);
+  rfx::ivf::launch_init_centroids(codes, n / m, m, D, iv->qc, st);
+  rfx::ivf::launch_centroid_update(nullptr, nullptr, m, D, iv->qc, iv->fc, st);
   for (int it = 0; it < iters && rc == RFX_OK; ++it) {
     if (rfx::ivf::launch_assign(codes, n, iv->qc, m, D, iv->fc, lab, nullptr, st)) {
       rc = api_fail(RFX_EUNSUPPORTED, "assignment launch rejected");

@@ -369,6 +369,22 @@ __global__ __launch_bounds__(256) void centroid_update_kernel(const int* __restr
   if (lane == 0) fc[c] = n2 > 0 ? cr_inv_sqrt_int((float)n2) : 0.f;
 }
 
+// initial centroids: qc_j = codes row j * step
+__global__ void init_centroids_kernel(const int8_t* __restrict__ codes, int64_t step, int m, int D,
+                                      int8_t* __restrict__ qc) {
+  const int64_t total = (int64_t)m * (D >> 4);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t j = i / (D >> 4), c = i - j * (D >> 4);
+    *(uint4*)(qc + j * D + c * 16) = *(const uint4*)(codes + j * step * D + c * 16);
+  }
+}
+
+void launch_init_centroids(const int8_t* codes, int64_t step, int m, int D, int8_t* qc, hipStream_t st) {
+  const int64_t total = (int64_t)m * (D >> 4);
+  hipLaunchKernelGGL(init_centroids_kernel, dim3((unsigned)std::min<int64_t>((total + 255) / 256, 4096)), dim3(256), 0,
+                     st, codes, step, m, D, qc);
+}
+
 void launch_kmeans_accum(const int8_t* X, int64_t n, int D, const int* labels, int* sums, int* counts,
                          hipStream_t st) {
   const int blocks = (int)std::min<int64_t>((std::max<int64_t>(n, 1) + 3) / 4, 8192);

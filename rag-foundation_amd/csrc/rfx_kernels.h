@@ -91,6 +91,7 @@ int launch_coarse_scores(const int8_t* X, int64_t n, const int8_t* C, int m, int
                          int* ids, hipStream_t st);
 int launch_assign(const int8_t* X, int64_t n, const int8_t* C, int m, int D, const float* fc, int* labels,
                   float* best, hipStream_t st);
+void launch_init_centroids(const int8_t* codes, int64_t step, int m, int D, int8_t* qc, hipStream_t st);
 void launch_kmeans_accum(const int8_t* X, int64_t n, int D, const int* labels, int* sums, int* counts,
                          hipStream_t st);
 // sums == nullptr: only recompute the factors of qc
