@@ -81,3 +81,40 @@ class ShardedSearch:
         cs, cr = self.index.scan(queries, k, workspace=workspace, stream=stream)
         rec = topk_merge_records(cs, cr, k, row_offset=self.row_offset, stream=stream)
         return gather_merge_records(rec, k, self.group, stream=stream)
+
+
+class ShardedIvf:
+    """Row-sharded IVF-Flat int8: every rank holds its rows' part of every
+    posting list under ONE coarse quantiser.  Rank 0 trains k-means on its sample and the int8
+    centroids are broadcast (nlist·dim bytes, once); each rank quantises/assigns its own rows.
+    A search is the brute-force path's exchange: local IVF top-k -> records with the rank's row
+    offset -> one all-gather -> rfx_merge_gathered."""
+
+    def __init__(self, ivf, row_offset: int, group=None):
+        self.ivf = ivf
+        self.row_offset = int(row_offset)
+        self.group = group
+
+    def train(self, sample: torch.Tensor = None, iters: int = 10, src: int = 0):
+        """Rank `src` trains on `sample`; the centroids reach every rank by broadcast."""
+        if dist.get_rank(self.group) == src:
+            self.ivf.train(sample, iters=iters)
+            qc = self.ivf.centroids()[0]
+        else:
+            qc = torch.empty((self.ivf.nlist, self.ivf.dim), dtype=torch.int8, device=self.ivf._dev())
+        if dist.get_world_size(self.group) > 1:
+            if dist.get_backend(self.group) == "gloo":
+                host = qc.cpu()
+                dist.broadcast(host, src=src, group=self.group)
+                qc = host.to(qc.device)
+            else:
+                dist.broadcast(qc, src=src, group=self.group)
+        if dist.get_rank(self.group) != src:
+            self.ivf.set_centroids(qc)
+
+    def search(self, queries: torch.Tensor, k: int, nprobe: int, workspace=None, stream=None):
+        from .index import topk_merge_records
+
+        s, r = self.ivf.search(queries, k, nprobe, workspace=workspace, stream=stream)
+        rec = topk_merge_records(s, r, k, row_offset=self.row_offset, stream=stream)
+        return gather_merge_records(rec, k, self.group, stream=stream)

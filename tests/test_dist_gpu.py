@@ -50,3 +50,39 @@ def test_sharded_gpu_search_equals_whole(world, n, nq, dtype, tmp_path):
     s, r, fs, fr = torch.load(out, weights_only=True)
     assert torch.equal(r, fr)
     assert torch.allclose(s, fs, atol=1e-6, rtol=0)
+
+
+def _ivf_worker(rank, world, port, n, nq, result):
+    import torch.distributed as dist
+
+    from rfx import dist as rdist
+    from rfx.ivf import IvfIndex, synth_clustered
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    dim, nlist = 256, 32
+    r0, r1 = rdist.shard_range(n, rank, world)
+    sh = rdist.ShardedIvf(IvfIndex(dim, nlist), r0)
+    sample = synth_clustered(7, 48, 5, 0, 2048, dim, "bf16") if rank == 0 else None
+    sh.train(sample, iters=3)
+    sh.ivf.add(synth_clustered(7, 48, 5, r0, r1 - r0, dim, "bf16"))
+    q = synth_clustered(7, 48, 99, 0, nq, dim, "bf16")
+    s, r = sh.search(q, 10, 6)
+    if rank == 0:
+        full = IvfIndex(dim, nlist)
+        full.train(sample, iters=3)
+        full.add(synth_clustered(7, 48, 5, 0, n, dim, "bf16"))
+        fs, fr = full.search(q, 10, 6)
+        torch.save((s.cpu(), r.cpu(), fs.cpu(), fr.cpu()), result)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_ivf_equals_whole(world, tmp_path):
+    # one quantiser trained on rank 0 and broadcast; each rank its rows' part of every list
+    out = str(tmp_path / "rank0.pt")
+    mp.start_processes(_ivf_worker, args=(world, _free_port(), 9000, 64, out), nprocs=world, start_method="spawn")
+    s, r, fs, fr = torch.load(out, weights_only=True)
+    assert torch.equal(r, fr) and torch.equal(s, fs)
