@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 #include <map>
 #include <memory>
@@ -133,8 +134,18 @@ int build(Ivf& iv, hipStream_t st) {
 
 size_t al256(size_t x) { return (x + 255) / 256 * 256; }
 
+// list-scan splits per list: enough (list, split) blocks to fill the chip several times over
+int ivf_splits(const Ivf& iv) {
+  if (const char* e = getenv("RFX_IVF_SPLITS")) {  // tuning override
+    const int v = atoi(e);
+    if (v >= 1 && v <= 64) return v;
+  }
+  const int64_t avg = iv.rows / std::max(iv.nlist, 1);
+  return avg >= 2048 ? 4 : (avg >= 512 ? 2 : 1);
+}
+
 struct IvfLayout {
-  int K;
+  int K, splits;
   int64_t ncand;
   size_t qq, qinv, S, Sid, ps, pid, poff, pairs, cs, cr, total;
 };
@@ -145,7 +156,8 @@ int ivf_layout(const Ivf& iv, int64_t nq, int k, int nprobe, IvfLayout& L) {
     return api_fail(RFX_EINVAL, "nprobe=%d out of range [1, min(64, nlist=%d)]", nprobe, iv.nlist);
   if (nq < 0 || nq * nprobe > (int64_t)INT32_MAX / 4) return api_fail(RFX_EINVAL, "nq=%lld out of range", (long long)nq);
   L.K = rfx::ivf::list_k(k);
-  L.ncand = (int64_t)nprobe * 4 * L.K;
+  L.splits = ivf_splits(iv);
+  L.ncand = (int64_t)nprobe * L.splits * 4 * L.K;
   size_t o = 0;
   L.qq = o, o += al256((size_t)nq * iv.dim);
   L.qinv = o, o += al256((size_t)nq * 4);
@@ -394,7 +406,7 @@ int rfx_ivf_search(rfx_ivf_t h, const void* queries_d, int64_t nq, int dtype, in
     return api_fail(RFX_EUNSUPPORTED, "probe selection rejected (nprobe=%d)", nprobe);
   if (rfx::ivf::launch_group_pairs(pid, (int)(nq * nprobe), iv->nlist, poff, pairs, st))
     return api_fail(RFX_EUNSUPPORTED, "pair grouping rejected");
-  if (rfx::ivf::launch_list_scan(L.K, iv->dim, iv->nlist, iv->lcodes, iv->linv, iv->lids, iv->off, poff, pairs, nprobe,
+  if (rfx::ivf::launch_list_scan(L.K, iv->dim, iv->nlist, L.splits, iv->lcodes, iv->linv, iv->lids, iv->off, poff, pairs, nprobe,
                                  qq, qinv, cs, cr, st))
     return api_fail(RFX_EUNSUPPORTED, "list scan launch rejected (k=%d dim=%d)", k, iv->dim);
   if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.ncand, 1, k, 0, out_scores_d, out_rows_d, nullptr, st))

@@ -516,10 +516,12 @@ __global__ __launch_bounds__(1024) void group_pairs_kernel(const int64_t* __rest
   for (int p = t; p < P; p += 1024) pairs[atomicAdd(&cnt[(int)probes[p]], 1)] = p;
 }
 
-// Posting-list scan.  One block per list; the queries probing it (pairs) in batches of QB staged
-// in LDS; every wave streams rows (16 lanes per row, 16-byte chunks j, j+16, ..), v_dot4_i32_i8
-// against each staged query, DPP row sum, and keeps one top-K list per query.  Candidates:
-// cand[(q * nprobe + j) * 4 + wave][K] (every pair of every list is written, empty lists too).
+// Posting-list scan.  Grid (list, split): block (L, s) takes the 64-row groups s*4 + w,
+// s*4 + w + 4*S, ... of list L (S splits balance long lists over the chip); the queries probing
+// it (pairs) in batches of QB staged in LDS; every wave streams rows (16 lanes per row, 16-byte
+// chunks j, j+16, ..), v_dot4_i32_i8 against each staged query, DPP row sum, and keeps one
+// top-K list per query.  Candidates: cand[((q * nprobe + j) * S + s) * 4 + wave][K] (every pair
+// of every list is written, empty lists too).
 constexpr int kQB = 8;
 template <int K, int NC>
 __global__ __launch_bounds__(256) void list_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ inv,
@@ -531,7 +533,7 @@ __global__ __launch_bounds__(256) void list_scan_kernel(const int8_t* __restrict
   constexpr int D = NC * 256;
   __shared__ __attribute__((aligned(16))) int8_t qs[kQB][D];
   __shared__ float qf[kQB];
-  const int L = blockIdx.x;
+  const int L = blockIdx.x, S = gridDim.y, sp = blockIdx.y;
   const int p0 = pair_off[L], p1 = pair_off[L + 1];
   if (p0 == p1) return;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, j = lane & 15;
@@ -549,7 +551,7 @@ __global__ __launch_bounds__(256) void list_scan_kernel(const int8_t* __restrict
     WaveList<K> lst[kQB];
 #pragma unroll
     for (int qi = 0; qi < kQB; ++qi) lst[qi].init();
-    for (int64_t base = r0 + (int64_t)w * 64; base < r1; base += 256) {
+    for (int64_t base = r0 + (int64_t)(sp * 4 + w) * 64; base < r1; base += 256 * S) {
       float cand[kQB];
 #pragma unroll
       for (int qi = 0; qi < kQB; ++qi) cand[qi] = 0.f;
@@ -590,7 +592,7 @@ __global__ __launch_bounds__(256) void list_scan_kernel(const int8_t* __restrict
 #pragma unroll
       for (int qi = 0; qi < kQB; ++qi) {
         if (qi < nb) {
-          const int64_t o = ((int64_t)pairs[pb + qi] * 4 + w) * K + lane;
+          const int64_t o = (((int64_t)pairs[pb + qi] * S + sp) * 4 + w) * K + lane;
           cand_s[o] = lst[qi].ls;
           cand_r[o] = lst[qi].lr;
         }
@@ -602,13 +604,13 @@ __global__ __launch_bounds__(256) void list_scan_kernel(const int8_t* __restrict
 
 int list_k(int k) { return k <= 4 ? 4 : (k <= 16 ? 16 : (k <= 64 ? 64 : -1)); }
 
-int launch_list_scan(int K, int D, int m, const int8_t* codes, const float* inv, const int* ids, const int64_t* off,
+int launch_list_scan(int K, int D, int m, int splits, const int8_t* codes, const float* inv, const int* ids, const int64_t* off,
                      const int* pair_off, const int* pairs, int nprobe, const int8_t* qq, const float* qinv,
                      float* cs, int* cr, hipStream_t st) {
 #define RFX_LS(KV, NCV)                                                                                     \
   if (K == KV && D == NCV * 256) {                                                                          \
-    hipLaunchKernelGGL((list_scan_kernel<KV, NCV>), dim3(m), dim3(256), 0, st, codes, inv, ids, off, pair_off, \
-                       pairs, nprobe, qq, qinv, cs, cr);                                                    \
+    hipLaunchKernelGGL((list_scan_kernel<KV, NCV>), dim3(m, splits), dim3(256), 0, st, codes, inv, ids, off,  \
+                       pair_off, pairs, nprobe, qq, qinv, cs, cr);                                          \
     return 0;                                                                                               \
   }
   RFX_LS(4, 1) RFX_LS(4, 2) RFX_LS(4, 3) RFX_LS(4, 4)

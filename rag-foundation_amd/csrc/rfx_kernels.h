@@ -103,7 +103,7 @@ int launch_build_lists(const int* labels, int64_t n, int m, const int8_t* codes,
                        hipStream_t st);
 int list_k(int k);
 int launch_group_pairs(const int64_t* probes, int P, int m, int* pair_off, int* pairs, hipStream_t st);
-int launch_list_scan(int K, int D, int m, const int8_t* codes, const float* inv, const int* ids, const int64_t* off,
+int launch_list_scan(int K, int D, int m, int splits, const int8_t* codes, const float* inv, const int* ids, const int64_t* off,
                      const int* pair_off, const int* pairs, int nprobe, const int8_t* qq, const float* qinv,
                      float* cs, int* cr, hipStream_t st);
 }  // namespace ivf
