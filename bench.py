@@ -87,7 +87,7 @@ def main():
     ix.add_synthetic(a.seed, n_local, gen_row0=r0)
     q = synth_rows(a.seed + 1, 0, a.nq, a.dim, a.dtype, local)
     kern, n_cand = ix.plan(a.nq, a.k)
-    list_len = 1  # single-pass merge (the list-heads prefilter measured slower)
+    list_len = ix.list_len(a.nq, a.k)  # sorted candidate lists: the merge bounds by their k-th entries
     rec = torch.empty((a.nq, a.k, 2), dtype=torch.int64, device=dev)
     ws = torch.empty(max(ix.workspace_bytes(a.nq, a.k), 1), dtype=torch.uint8, device=dev)
     cs = torch.empty((a.nq, n_cand), dtype=torch.float32, device=dev)

@@ -82,7 +82,7 @@ void launch_nan_rows(void* X, const int64_t* rows_d, int64_t n, int64_t row_byte
 // VALU fused scan + top-k (nq <= 8 per launch slice).
 //   X      : [nrows][D] dtype DT
 //   Qf     : [nq][D] f32 (exact widening of the index-dtype queries)
-//   output : cand_s/cand_r [nq][n_lists][K], n_lists = gridDim.x * 4 (one list per wave)
+//   output : cand_s/cand_r [nq][n_lists][K], n_lists = gridDim.x (the 4 wave lists merged per block)
 // Algorithmic bytes per row: D * esz (the row is read once for all NQT queries).
 // ---------------------------------------------------------------------------------------
 template <int DT>
@@ -102,7 +102,8 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
                                                         const float* __restrict__ Qf, int nq,
                                                         int rows_per_wave, float* __restrict__ cand_s,
                                                         int* __restrict__ cand_r, int n_lists,
-                                                        const uint32_t* __restrict__ mask) {
+                                                        const uint32_t* __restrict__ mask,
+                                                        uint32_t* __restrict__ tau) {
   constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
   constexpr int EPV = 16 / ESZ;
   extern __shared__ __attribute__((aligned(16))) float q_lds[];  // [NQT][D]
@@ -183,14 +184,43 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
     for (int qi = 0; qi < NQT; ++qi) L[qi].offer(cand[qi], crow, ok);
   }
 
+  // block-level merge: the 4 wave lists of a query -> one list per block (4x fewer candidates
+  // for the merge kernel, which dominates single-query latency); wave w merges queries w, w+4, ..
+  __shared__ float ms[4][NQT][K];
+  __shared__ int mr[4][NQT][K];
+  const int w = tid >> 6;
   if (lane < K) {
 #pragma unroll
     for (int qi = 0; qi < NQT; ++qi) {
-      if (qi < nqt) {
-        const int64_t o = ((int64_t)(q0 + qi) * n_lists + wave_g) * K + lane;
-        cand_s[o] = L[qi].ls;
-        cand_r[o] = L[qi].lr;
-      }
+      ms[w][qi][lane] = L[qi].ls;
+      mr[w][qi][lane] = L[qi].lr;
+    }
+  }
+  __syncthreads();
+  for (int qi = w; qi < nqt; qi += 4) {
+    WaveList<K> M;
+    M.init();
+#pragma unroll
+    for (int src = 0; src < 4; ++src) {
+      const bool v = lane < K;
+      M.offer(v ? ms[src][qi][lane] : -__builtin_inff(), v ? mr[src][qi][lane] : kEmptyRow,
+              v && mr[src][qi][lane] != kEmptyRow);
+    }
+    // cross-block pruning: every block's K-th best is a lower bound of the query's K-th best
+    // (>= its k-th best), so entries below the running max of those bounds can never be
+    // returned; write them as empty (the merge skips them without an insert).
+    uint32_t bound = 0u;
+    if (tau) {
+      const float kth = readlane_f(M.ls, K - 1);
+      const uint32_t mine = kth > -__builtin_inff() ? ord_f32(kth) : 0u;
+      if (lane == 0) bound = atomicMax(tau + q0 + qi, mine);
+      bound = max((uint32_t)__builtin_amdgcn_readfirstlane(bound), mine);
+    }
+    if (lane < K) {
+      const int64_t o = ((int64_t)(q0 + qi) * n_lists + blockIdx.x) * K + lane;
+      const bool keep = M.lr != kEmptyRow && ord_f32(M.ls) >= bound;
+      cand_s[o] = keep ? M.ls : -__builtin_inff();
+      cand_r[o] = keep ? M.lr : kEmptyRow;
     }
   }
 }
@@ -202,11 +232,11 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
 template <int DT, int NQT, int K>
 static int launch_valu_vpl(int vpl, dim3 grid, size_t lds, hipStream_t st, const uint8_t* X, int nrows,
                            int D, const float* Qf, int nq, int rpw, float* cs, int* cr, int n_lists,
-                           const uint32_t* mask) {
+                           const uint32_t* mask, uint32_t* tau) {
 #define RFX_L(V)                                                                                  \
   if (vpl <= V) {                                                                                 \
     hipLaunchKernelGGL((scan_valu_kernel<DT, NQT, K, V>), grid, dim3(256), lds, st, X, nrows, D, Qf, \
-                       nq, rpw, cs, cr, n_lists, mask);                                           \
+                       nq, rpw, cs, cr, n_lists, mask, tau);                                      \
     return 0;                                                                                     \
   }
   RFX_L(4) RFX_L(8) RFX_L(12) RFX_L(16)
@@ -217,9 +247,9 @@ static int launch_valu_vpl(int vpl, dim3 grid, size_t lds, hipStream_t st, const
 template <int DT, int NQT>
 static int launch_valu_k(int kk, int vpl, dim3 grid, size_t lds, hipStream_t st, const uint8_t* X,
                          int nrows, int D, const float* Qf, int nq, int rpw, float* cs, int* cr,
-                         int n_lists, const uint32_t* mask) {
+                         int n_lists, const uint32_t* mask, uint32_t* tau) {
 #define RFX_K(KV) \
-  if (kk == KV) return launch_valu_vpl<DT, NQT, KV>(vpl, grid, lds, st, X, nrows, D, Qf, nq, rpw, cs, cr, n_lists, mask);
+  if (kk == KV) return launch_valu_vpl<DT, NQT, KV>(vpl, grid, lds, st, X, nrows, D, Qf, nq, rpw, cs, cr, n_lists, mask, tau);
   RFX_VALU_K_LIST(RFX_K)
 #undef RFX_K
   return -1;
@@ -243,13 +273,13 @@ ValuPlan plan_scan_valu(int64_t nrows, int D, int dtype, int64_t nq, int k) {
   if (waves < 1) waves = 1;
   p.rows_per_wave = (int)rpw;
   p.blocks = (int)((waves + 3) / 4);
-  p.n_lists = p.blocks * 4;
+  p.n_lists = p.blocks;  // one merged list per block
   p.ok = p.vpl <= 16 && p.k_slot <= 64 && (int64_t)D * esz % 16 == 0;
   return p;
 }
 
 int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dtype, const float* Qf,
-                     int nq, float* cs, int* cr, hipStream_t st, const uint32_t* mask) {
+                     int nq, float* cs, int* cr, hipStream_t st, const uint32_t* mask, uint32_t* tau) {
   dim3 grid(p.blocks, p.q_slices);
   const size_t lds = (size_t)p.nqt * D * sizeof(float);
   const uint8_t* Xb = (const uint8_t*)X;
@@ -257,12 +287,12 @@ int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dty
   if (p.nqt == NQV) {                                                                              \
     if (dtype == RFX_F32)                                                                          \
       return launch_valu_k<RFX_F32, NQV>(p.k_slot, p.vpl, grid, lds, st, Xb, nrows, D, Qf, nq,       \
-                                         p.rows_per_wave, cs, cr, p.n_lists, mask);                      \
+                                         p.rows_per_wave, cs, cr, p.n_lists, mask, tau);                      \
     if (dtype == RFX_BF16)                                                                         \
       return launch_valu_k<RFX_BF16, NQV>(p.k_slot, p.vpl, grid, lds, st, Xb, nrows, D, Qf, nq,      \
-                                          p.rows_per_wave, cs, cr, p.n_lists, mask);                     \
+                                          p.rows_per_wave, cs, cr, p.n_lists, mask, tau);                     \
     return launch_valu_k<RFX_F16, NQV>(p.k_slot, p.vpl, grid, lds, st, Xb, nrows, D, Qf, nq,         \
-                                       p.rows_per_wave, cs, cr, p.n_lists, mask);                        \
+                                       p.rows_per_wave, cs, cr, p.n_lists, mask, tau);                        \
   }
   RFX_NQ(1) RFX_NQ(4) RFX_NQ(8)
 #undef RFX_NQ
@@ -284,7 +314,10 @@ void launch_stream_read(const void* p, int64_t bytes, uint32_t* out, hipStream_t
 }
 
 // Widen index-dtype queries to f32 (exact).
-__global__ void widen_queries_kernel(const void* __restrict__ Q, int64_t n, int dtype, float* __restrict__ out) {
+__global__ void widen_queries_kernel(const void* __restrict__ Q, int64_t n, int dtype, float* __restrict__ out,
+                                     uint32_t* __restrict__ tau, int64_t n_tau) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_tau; i += (int64_t)gridDim.x * blockDim.x)
+    tau[i] = 0u;  // the scan's per-query pruning bounds start empty
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     if (dtype == RFX_F32)
       out[i] = ((const float*)Q)[i];
@@ -295,21 +328,20 @@ __global__ void widen_queries_kernel(const void* __restrict__ Q, int64_t n, int 
   }
 }
 
-void launch_widen_queries(const void* Q, int64_t n, int dtype, float* out, hipStream_t st) {
+void launch_widen_queries(const void* Q, int64_t n, int dtype, float* out, hipStream_t st, uint32_t* tau,
+                          int64_t n_tau) {
   const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(widen_queries_kernel, dim3(blocks < 1 ? 1 : blocks), dim3(256), 0, st, Q, n, dtype, out);
+  hipLaunchKernelGGL(widen_queries_kernel, dim3(blocks < 1 ? 1 : blocks), dim3(256), 0, st, Q, n, dtype, out, tau,
+                     tau ? n_tau : 0);
 }
 
 // ---------------------------------------------------------------------------------------
 // Top-k merge: one 512-thread block per query.  The candidates of a query are groups of
-// `list_len` (the scan kernels' sorted partial lists; list_len = 1: no structure).
-//   pass 1: the 8 waves fold the list HEADS (each list's first entry) into wave lists; wave 0
-//           merges them into H = top-K of the heads.  T = H's K-th entry.
-//   pass 2: every other candidate enters a wave list only if it beats T (one ballot per 64
-//           candidates; with sorted lists almost everything is rejected there).
-//   final:  wave 0 merges H and the 8 pass-2 lists.
-// Exact for any grouping: H holds K distinct candidates >= T, so every candidate of the final
-// top-K that is not a head beats T strictly (rows are distinct, ties break on the row id).
+// `list_len` (the scan kernels' sorted partial lists, best first; list_len = 1: no structure).
+//   bound:  with list_len >= k, T = max over lists of the min of the list's first k entries (a
+//           lower bound of the query's k-th best); the wave lists admit only scores >= T.
+//   pass:   the 8 waves fold every candidate (one ballot per 64; below T nothing is inserted);
+//   final:  rank_merge of the 8 wave lists.
 // Sources: flat [nq][n_cand] (score, row) arrays, or the all-gathered per-rank records of the
 // multi-GPU path ([world][nq][k] of {f32 score, pad, i64 row}).
 // ---------------------------------------------------------------------------------------
@@ -371,20 +403,6 @@ __device__ __forceinline__ void merge_chunk(const Src& src, int64_t q, int64_t b
   }
 }
 
-// One head (list_len-strided candidate) per lane.
-template <int K, bool R64, class Src>
-__device__ __forceinline__ void merge_heads(const Src& src, int64_t q, int64_t nh, int list_len, int w, int lane,
-                                            WaveList64<K>& L) {
-  for (int64_t b = (int64_t)w * 64; b < nh; b += 8 * 64) {
-    const int64_t h = b + lane;
-    float sc = -__builtin_inff();
-    long long rr = kNoRow;
-    if (h < nh) src.get(q, h * list_len, sc, rr);
-    const bool live = rr >= 0 && rr != kNoRow && (R64 || rr != (long long)kEmptyRow);
-    L.offer(sc, rr, live);
-  }
-}
-
 // Block-wide merge of M sorted lists of K (best first, padded with (-inf, kNoRow)) in LDS into the
 // top-K list `dst` (pre-filled with padding by the caller): every thread takes candidates and
 // computes their rank as its index plus, for each other list, the number of entries better than
@@ -428,43 +446,60 @@ __global__ __launch_bounds__(512) void merge_kernel(Src src, int list_len, int k
   const int64_t q = blockIdx.x;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int64_t n = src.n;
-  const int64_t nh = list_len > 1 ? n / list_len : n;  // heads
   constexpr int P = 8;  // chunk: 8 * 512 candidates per block
   if (tid < 2 * K) {
     ls_lds[8 + tid / K][tid % K] = -__builtin_inff();
     lr_lds[8 + tid / K][tid % K] = kNoRow;
   }
-  // ---- pass 1: heads (list_len == 1: every candidate is a head) ----
+  // ---- bound: with lists of list_len >= k_out entries, the minimum of a list's first k_out
+  // entries is a lower bound of the query's k_out-th best (that list alone holds k_out candidates
+  // at or above it; for the scan's sorted lists it is the k_out-th entry), so the max over lists
+  // T only admits what can still be returned — exact whether or not the lists are sorted ----
   WaveList64<K> L;
   L.init();
-  if (list_len > 1) {
-    merge_heads<K, R64>(src, q, nh, list_len, w, lane, L);
-  } else {
-    for (int64_t base = (int64_t)w * 64; base < n; base += (int64_t)P * 8 * 64)
-      merge_chunk<K, R64, P>(src, q, base, n, lane, 1, false, L);
+  if (list_len > 1 && list_len >= k_out) {
+    __shared__ uint32_t tb;
+    if (tid == 0) tb = 0u;
+    __syncthreads();
+    uint32_t m = 0u;
+    for (int64_t j = tid; j < n / list_len; j += 512) {
+      uint32_t mj = 0xffffffffu;  // min over the list's first k_out entries (sorted or not)
+      for (int e0 = 0; e0 < k_out; e0 += 8) {  // 8 independent loads in flight per round
+        float sc[8];
+        long long rr[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          sc[u] = __builtin_inff();
+          rr[u] = 0;
+          if (e0 + u < k_out) src.get(q, j * list_len + e0 + u, sc[u], rr[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const bool live = rr[u] >= 0 && rr[u] != kNoRow && (R64 || rr[u] != (long long)kEmptyRow);
+          mj = min(mj, live ? ord_f32(sc[u]) : 0u);
+        }
+      }
+      m = max(m, mj);
+    }
+#pragma unroll
+    for (int off = 32; off; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
+    if (lane == 0) atomicMax(&tb, m);
+    __syncthreads();
+    if (tb) {
+      const uint32_t u = tb & 0x80000000u ? tb & 0x7fffffffu : ~tb;  // inverse of ord_f32
+      L.init_above(__uint_as_float(u), kNoRow);                      // admits score >= T
+    }
   }
+  for (int64_t base = (int64_t)w * 64; base < n; base += (int64_t)P * 8 * 64)
+    merge_chunk<K, R64, P>(src, q, base, n, lane, 1, false, L);
   if (lane < K) {
     ls_lds[w][lane] = L.ls;
     lr_lds[w][lane] = L.lr;
   }
   __syncthreads();
-  rank_merge<K, 8>(ls_lds, lr_lds, ls_lds[8], lr_lds[8]);  // H
+  rank_merge<K, 8>(ls_lds, lr_lds, ls_lds[8], lr_lds[8]);
   __syncthreads();
-  int fin = 8;
-  // ---- pass 2: the rest, admitted only above T = H's K-th entry ----
-  if (list_len > 1) {
-    L.init_above(ls_lds[8][K - 1], lr_lds[8][K - 1]);
-    for (int64_t base = (int64_t)w * 64; base < n; base += (int64_t)P * 8 * 64)
-      merge_chunk<K, R64, P>(src, q, base, n, lane, list_len, true, L);
-    if (lane < K) {  // rows 0..7 were last read by the rank_merge above (a barrier ago)
-      ls_lds[w][lane] = L.ls;
-      lr_lds[w][lane] = L.lr;
-    }
-    __syncthreads();
-    rank_merge<K, 9>(ls_lds, lr_lds, ls_lds[9], lr_lds[9]);
-    __syncthreads();
-    fin = 9;
-  }
+  const int fin = 8;
   if (tid < k_out) {
     const long long rr = lr_lds[fin][tid];
     const bool empty = rr == kNoRow;

@@ -150,6 +150,7 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
     if (!L.vp.ok) return fail(RFX_EUNSUPPORTED, "no scan kernel for dim=%d dtype=%d k=%d", ix.dim, ix.dtype, k);
     L.n_cand = (int64_t)L.vp.n_lists * L.vp.k_slot;
     L.q_bytes = (size_t)nq * ix.dim * 4;
+    tau_bytes = (size_t)nq * 4;  // per-query pruning bounds of the VALU scan
   }
   if (ix.rows == 0) L.n_cand = 0;
   L.q_off = 0;
@@ -182,8 +183,9 @@ int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq,
     if (rc != 0) return fail(RFX_EUNSUPPORTED, "MFMA scan launch rejected (%d)", rc);
   } else {
     float* qf = (float*)(ws + L.q_off);
-    rfx::launch_widen_queries(queries, nq * ix.dim, ix.dtype, qf, st);
-    if (rfx::launch_scan_valu(L.vp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qf, (int)nq, cs, cr, st, mask) != 0)
+    uint32_t* tau = (uint32_t*)(ws + L.tau_off);
+    rfx::launch_widen_queries(queries, nq * ix.dim, ix.dtype, qf, st, tau, nq);
+    if (rfx::launch_scan_valu(L.vp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qf, (int)nq, cs, cr, st, mask, tau) != 0)
       return fail(RFX_EUNSUPPORTED, "VALU scan launch rejected");
   }
   RFX_HIP(hipGetLastError());
@@ -645,9 +647,9 @@ int rfx_search_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k, c
   int32_t* cr = (int32_t*)(ws + L.cr_off);
   rc = scan_into(*ix, L, queries_d, nq, cs, cr, ws, st, row_mask_d);
   if (rc) return rc;
-  // one pass over all candidates: the list-heads prefilter (list_len > 1) measured slower on the
-  // scan's output (14 vs 19 us at 256 x 5120 candidates, tools/merge_bench.py)
-  if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.n_cand, 1, k, 0, out_scores_d, out_rows_d, nullptr, st) != 0)
+  // the scan's candidates are sorted lists: the merge bounds admission by the lists' k-th entries
+  const int list_len = L.kernel ? L.mp.k_lane : L.vp.k_slot;
+  if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.n_cand, list_len, k, 0, out_scores_d, out_rows_d, nullptr, st) != 0)
     return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
   RFX_HIP(hipGetLastError());
   return RFX_OK;

@@ -18,6 +18,12 @@ __device__ __forceinline__ bool better64(float s1, long long r1, float s2, long 
   return s1 > s2 || (s1 == s2 && r1 < r2);
 }
 
+// orderable u32 of a non-NaN float (larger float -> larger key; 0 stays below every score key)
+__device__ __forceinline__ uint32_t ord_f32(float s) {
+  const uint32_t u = __float_as_uint(s);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
 // ---- row masks (metadata filters): bit (r & 31) of word r >> 5 set = row r may be returned ------
 // A lane of a 32x32 MFMA accumulator holds rows rb + (r & 3) + 8 (r >> 2), r < 16, with
 // rb ≡ 0 or 4 (mod 32): all in word rb >> 5.  acc_row_bits puts row (r & 3) + 8 (r >> 2) of the

@@ -14,7 +14,9 @@ void launch_synth_rows(uint64_t seed, int64_t row0, int64_t n, int dim, int dtyp
 void launch_nan_rows(void* X, const int64_t* rows_d, int64_t n, int64_t row_bytes, int dtype,
                      hipStream_t st);
 void launch_stream_read(const void* p, int64_t bytes, uint32_t* out, hipStream_t st);
-void launch_widen_queries(const void* Q, int64_t n, int dtype, float* out, hipStream_t st);
+// also zeroes tau[0..n_tau) (the VALU scan's per-query pruning bounds) when tau != nullptr
+void launch_widen_queries(const void* Q, int64_t n, int dtype, float* out, hipStream_t st, uint32_t* tau = nullptr,
+                          int64_t n_tau = 0);
 
 // ---- VALU scan (small nq) ------------------------------------------------------------------
 struct ValuPlan {
@@ -25,8 +27,10 @@ int valu_k_slot(int k);
 ValuPlan plan_scan_valu(int64_t nrows, int D, int dtype, int64_t nq, int k);
 // mask (every scan launcher): optional row mask, bit (r & 31) of word r >> 5 set = row r may be
 // returned, (nrows + 31) / 32 words; nullptr = all rows (the production kernels run unchanged).
+// tau: optional [nq] u32 pruning bounds, zeroed beforehand (launch_widen_queries)
 int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dtype, const float* Qf,
-                     int nq, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
+                     int nq, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr,
+                     uint32_t* tau = nullptr);
 
 // ---- MFMA scan (batched bf16 / f16) -------------------------------------------------------
 struct MfmaPlan {

@@ -79,7 +79,8 @@ class ShardedSearch:
         from .index import topk_merge_records
 
         cs, cr = self.index.scan(queries, k, workspace=workspace, stream=stream)
-        rec = topk_merge_records(cs, cr, k, row_offset=self.row_offset, stream=stream)
+        rec = topk_merge_records(cs, cr, k, row_offset=self.row_offset, stream=stream,
+                                 list_len=self.index.list_len(queries.shape[0], k))
         return gather_merge_records(rec, k, self.group, stream=stream)
 
 
