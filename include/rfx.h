@@ -125,10 +125,10 @@ int rfx_scan_topk_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k
 int rfx_topk_merge(const float* cand_scores_d, const void* cand_rows_d, int rows_are_i64,
                    int64_t nq, int64_t n_cand, int k, int64_t row_offset, float* out_scores_d,
                    int64_t* out_rows_d, void* stream);
-/* Same, told that the candidates of a query are sorted lists of list_len entries (best first), as
- * rfx_scan_topk writes them (rfx_scan_list_len): the merge first takes the top-k of the list
- * heads and then admits only candidates above its k-th entry.  Any list_len gives the exact
- * result; a wrong one only costs time. */
+/* Same, told that the candidates of a query are lists of list_len entries (rfx_scan_topk writes
+ * sorted lists of rfx_scan_list_len entries): with list_len >= k the merge only admits scores at
+ * or above the max over lists of each list's minimum among its first k entries, a lower bound of
+ * the k-th best.  Exact for any list_len, sorted or not; a wrong one only costs time. */
 int rfx_scan_list_len(rfx_index_t h, int64_t nq, int k, int* out_list_len);
 int rfx_topk_merge_lists(const float* cand_scores_d, const void* cand_rows_d, int rows_are_i64,
                          int64_t nq, int64_t n_cand, int list_len, int k, int64_t row_offset,
