@@ -68,7 +68,16 @@ constexpr int kTauW = 16;                 // u32 per query in the threshold tabl
 // bound sends more lanes into the insert path), so the table is refreshed every 4 tiles throughout.
 // (MODE 524288, diagnostic: every 2nd tile.  The vmcnt windows below allow refresh tiles >= 2 apart.)
 template <int MODE>
-__device__ __forceinline__ bool tau_refresh_tile(int it) { return (MODE & 524288) ? (it & 1) == 1 : (it & 3) == 3; }
+__device__ __forceinline__ bool tau_refresh_tile(int it) {
+  // production: right after tiles 0 and 1 (the lists start empty, so the first tiles take the
+  // slow insert path until the slot table's bound arrives: 2x fewer slow entries, -13 us per
+  // launch at 8 tiles per block, tools/early_refresh.py), then every 4 tiles.
+  // MODE 4194304: every 4 tiles only; 8388608: also after tile 2; 524288: every 2 tiles.
+  if constexpr ((MODE & 8388608) != 0) return it < 4 || (it & 3) == 3;
+  if constexpr ((MODE & 4194304) != 0) return (it & 3) == 3;
+  if constexpr ((MODE & 524288) != 0) return (it & 1) == 1;
+  return it < 2 || (it & 3) == 3;
+}
 constexpr int kTauOff = kRing * kSlot;    // 96 KB
 constexpr int kTauBytes = kQG * kTauW * 4;  // 16 KB: 16 DMA wave-instructions, 2 per wave
 constexpr int kTauGPW = kTauBytes / 1024 / kWaves;
@@ -261,7 +270,8 @@ __global__ __launch_bounds__(512, 1) void scan_mfma5_kernel(const uint16_t* __re
     }
     // A threshold refresh (kTauGPW ops) issued after the barrier of stage g_r = last stage of a
     // refresh tile it_r is younger than stage g+1's pieces iff g-4 <= g_r <= g-1: at every stage
-    // of tile it_r + 1 and at stage 0 of tile it_r + 2 (refresh tiles are >= 4 apart).
+    // of tile it_r + 1 and at stage 0 of tile it_r + 2.  Where two refreshes overlap (tiles 0, 1)
+    // the count below admits one: the wait is then stricter than needed, never looser.
     const bool tau_young12 = it >= 1 && tau_refresh_tile<MODE>(it - 1);
     const bool tau_young0 = tau_young12 || (it >= 2 && tau_refresh_tile<MODE>(it - 2));
 #pragma unroll

@@ -591,7 +591,7 @@ int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k
   void* qpad = (uint8_t*)ws_d + L.q_off;
   rfx::launch_pad_queries(queries_d, nq, L.mp.nq_pad, ix->dim, 2, qpad, st);
   int rc2;
-  if (mode >= 1000 && mode < 4000000)  // two-waves-per-SIMD kernel ablations: mode 1000 + MODE
+  if (mode >= 1000 && mode < 16000000)  // two-waves-per-SIMD kernel ablations: mode 1000 + MODE
     rc2 = rfx::launch_scan_mfma5_dbg(rfx::plan_scan_mfma5(ix->rows, ix->dim, ix->dtype, nq, k), mode - 1000, ix->data,
                                      (int)ix->rows, ix->dtype, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st);
   else if (mode >= 20 && mode < 1000)  // all-query-stationary kernel ablations: mode 20 + MODE
