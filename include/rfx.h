@@ -209,6 +209,16 @@ int rfx_ivf_search_workspace_bytes(rfx_ivf_t h, int64_t nq, int k, int nprobe, s
 int rfx_ivf_search(rfx_ivf_t h, const void* queries_d, int64_t nq, int dtype, int k, int nprobe,
                    float* out_scores_d, int64_t* out_rows_d, void* ws_d, size_t ws_bytes,
                    void* stream);
+/* Search + exact re-rank: the IVF keeps rerank_k (k <= rerank_k <= 64) candidates per query by
+ * int8 score, each is re-scored in f32 against its original row (rows_d [rows][dim] of rows_dtype
+ * in insertion order, e.g. rfx_index_data of a brute-force store holding the same rows), and the
+ * top k are returned (score desc, row asc).  Lifts recall@10 above the int8 ceiling. */
+int rfx_ivf_rerank_workspace_bytes(rfx_ivf_t h, int64_t nq, int k, int nprobe, int rerank_k,
+                                   size_t* out_bytes);
+int rfx_ivf_search_rerank(rfx_ivf_t h, const void* queries_d, int64_t nq, int dtype, int k,
+                          int nprobe, int rerank_k, const void* rows_d, int rows_dtype,
+                          float* out_scores_d, int64_t* out_rows_d, void* ws_d, size_t ws_bytes,
+                          void* stream);
 /* int8 quantisation of rows (the IVF code format): codes [n][dim], inv [n] = amax / 127 */
 int rfx_quantize(const void* rows_d, int64_t n, int dim, int dtype, int8_t* codes_d, float* inv_d,
                  void* stream);

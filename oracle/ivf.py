@@ -131,6 +131,23 @@ def search(qq, qinv, codes, inv, labels, qc, fc, nprobe: int, k: int, probe_ids=
     return out_s, out_r
 
 
+def rerank(cand_rows: np.ndarray, q64: np.ndarray, rows64: np.ndarray, k: int):
+    """Exact re-rank of IVF candidates [nq][kc] (rows, -1 = padding) against the original rows:
+    f64 dot, then top-k by (score desc, row asc), padded (-inf, -1)."""
+    nq = cand_rows.shape[0]
+    out_s = np.full((nq, k), -np.inf)
+    out_r = np.full((nq, k), -1, dtype=np.int64)
+    for i in range(nq):
+        rr = cand_rows[i][cand_rows[i] >= 0]
+        if len(rr) == 0:
+            continue
+        sc = rows64[rr] @ q64[i]
+        o = np.lexsort((rr, -sc))[:k]
+        out_s[i, :len(o)] = sc[o]
+        out_r[i, :len(o)] = rr[o]
+    return out_s, out_r
+
+
 # ---- clustered synthetic corpus (k_ivf.hip synth_clustered_kernel) ------------------------------
 C_KEY = 1 << 63   # key space of cluster centres
 L_KEY = 1 << 62   # key space of the row -> cluster draw

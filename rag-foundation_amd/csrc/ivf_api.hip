@@ -415,4 +415,47 @@ int rfx_ivf_search(rfx_ivf_t h, const void* queries_d, int64_t nq, int dtype, in
   return RFX_OK;
 }
 
+// Search with exact re-rank: the IVF search keeps rerank_k (>= k) candidates per query by int8
+// score, then every candidate is re-scored against its original row (rows_d: [rows][dim] of
+// rows_dtype in insertion order, e.g. rfx_index_data of the brute-force store holding the same
+// rows) in f32, and the merge keeps the top k.  Workspace: rfx_ivf_rerank_workspace_bytes.
+int rfx_ivf_rerank_workspace_bytes(rfx_ivf_t h, int64_t nq, int k, int nprobe, int rerank_k, size_t* out_bytes) {
+  if (rerank_k < k || rerank_k > 64) return api_fail(RFX_EINVAL, "rerank_k=%d must be in [k=%d, 64]", rerank_k, k);
+  size_t ivf = 0;
+  int rc = rfx_ivf_search_workspace_bytes(h, nq, rerank_k, nprobe, &ivf);
+  if (rc) return rc;
+  if (!out_bytes) return api_fail(RFX_EINVAL, "null out");
+  *out_bytes = al256(ivf) + 3 * al256((size_t)nq * rerank_k * 8);
+  return RFX_OK;
+}
+
+int rfx_ivf_search_rerank(rfx_ivf_t h, const void* queries_d, int64_t nq, int dtype, int k, int nprobe, int rerank_k,
+                          const void* rows_d, int rows_dtype, float* out_scores_d, int64_t* out_rows_d, void* ws_d,
+                          size_t ws_bytes, void* stream) {
+  auto iv = get(h);
+  if (!iv) return api_fail(RFX_EINVAL, "unknown IVF handle");
+  if (!valid_dtype(rows_dtype) || !valid_dtype(dtype)) return api_fail(RFX_EINVAL, "bad dtype");
+  size_t need = 0, ivf = 0;
+  int rc = rfx_ivf_rerank_workspace_bytes(h, nq, k, nprobe, rerank_k, &need);
+  if (rc) return rc;
+  if (nq == 0) return RFX_OK;
+  if (!rows_d || !queries_d || !out_scores_d || !out_rows_d) return api_fail(RFX_EINVAL, "null pointers");
+  if (!ws_d || ws_bytes < need) return api_fail(RFX_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, need);
+  rfx_ivf_search_workspace_bytes(h, nq, rerank_k, nprobe, &ivf);
+  uint8_t* ws = (uint8_t*)ws_d;
+  float* cs = (float*)(ws + al256(ivf));
+  int64_t* cr = (int64_t*)(ws + al256(ivf) + al256((size_t)nq * rerank_k * 8));
+  float* rs = (float*)(ws + al256(ivf) + 2 * al256((size_t)nq * rerank_k * 8));
+  int64_t* rr = cr;  // the re-rank kernel rewrites rows in place (padding -> empty sentinel)
+  if ((rc = rfx_ivf_search(h, queries_d, nq, dtype, rerank_k, nprobe, cs, cr, ws, al256(ivf), stream))) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  IVF_HIP(hipSetDevice(iv->device));
+  if (rfx::ivf::launch_rerank(queries_d, dtype, rows_d, rows_dtype, iv->dim, cr, nq, rerank_k, rs, rr, st))
+    return api_fail(RFX_EUNSUPPORTED, "re-rank launch rejected");
+  if (rfx::launch_topk_merge(rs, rr, 1, nq, rerank_k, k, 0, out_scores_d, out_rows_d, st))
+    return api_fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
+  IVF_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
 }  // extern "C"

@@ -129,6 +129,32 @@ class IvfIndex:
                                      ptr(ws), ws.numel(), stream_ptr(stream)))
         return out_s, out_r
 
+    def search_rerank(self, queries: torch.Tensor, k: int, nprobe: int, rows: torch.Tensor, rerank_k: int = None,
+                      stream=None):
+        """IVF search keeping rerank_k candidates (default max(k, 16): lists of up to 16 keep the
+        fast scan template), re-scored in f32 against the original rows [rows][dim] (insertion
+        order, e.g. DeviceIndex.read / the brute-force store)."""
+        q, dt = self._rows(queries)
+        if rows.dim() != 2 or rows.shape[1] != self.dim or rows.device != self._dev() or not rows.is_contiguous():
+            raise ValueError(f"rows must be a contiguous [n][{self.dim}] tensor on {self._dev()}")
+        if rows.shape[0] < self.rows:
+            raise ValueError(f"rows holds {rows.shape[0]} rows, the index {self.rows}")
+        rdt = {v: k_ for k_, v in _lib.TORCH_DTYPES.items()}.get(rows.dtype)
+        if rdt is None:
+            raise ValueError("rows must be float32, bfloat16 or float16")
+        rk = max(int(k), 16) if rerank_k is None else int(rerank_k)
+        nq = q.shape[0]
+        out_s = torch.empty((nq, k), dtype=torch.float32, device=self._dev())
+        out_r = torch.empty((nq, k), dtype=torch.int64, device=self._dev())
+        b = ctypes.c_size_t()
+        check(lib.rfx_ivf_rerank_workspace_bytes(self.handle, nq, int(k), int(nprobe), rk, ctypes.byref(b)))
+        ws = torch.empty(max(b.value, 1), dtype=torch.uint8, device=self._dev())
+        with torch.cuda.device(self.device):
+            check(lib.rfx_ivf_search_rerank(self.handle, ptr(q), nq, dt, int(k), int(nprobe), rk, ptr(rows),
+                                            _lib.DTYPE_CODES[rdt], ptr(out_s), ptr(out_r), ptr(ws), ws.numel(),
+                                            stream_ptr(stream)))
+        return out_s, out_r
+
 
 def quantize(rows: torch.Tensor, stream=None):
     """int8 codes [n][dim] + inv scales [n] of rows (the IVF code format)."""

@@ -166,3 +166,41 @@ def test_validation(rivf):
         ix.search(x, 10, 17)  # nprobe > nlist
     with pytest.raises(ValueError):
         ix.search(x, 65, 4)
+
+
+@pytest.mark.parametrize("rows_dtype", ["bf16", "f32"])
+def test_search_rerank_matches_oracle(rivf, rows_dtype):
+    # IVF candidates (bit-exact int8 stage) re-scored against the original rows: same rows as
+    # the oracle's f64 re-rank except inside the fp32 tie band, scores within 1e-5
+    dim, nlist, k, rk, nprobe = 768, 64, 10, 40, 8
+    rows = rivf.synth_clustered(7, 48, 5, 0, 8000, dim, rows_dtype)
+    ix = rivf.IvfIndex(dim, nlist)
+    ix.train(rows[::2].contiguous(), iters=4)
+    ix.add(rows)
+    q = rivf.synth_clustered(7, 48, 91, 0, 64, dim, "bf16")
+    s, r = ix.search_rerank(q, k, nprobe, rows, rerank_k=rk)
+    _, cand = ix.search(q, rk, nprobe)
+    rows64 = oivf.stored_to_f32(to_np(rows, rows_dtype), rows_dtype).astype(np.float64)
+    q64 = oivf.stored_to_f32(to_np(q, "bf16"), "bf16").astype(np.float64)
+    ref_s, ref_r = oivf.rerank(cand.cpu().numpy(), q64, rows64, k)
+    probs = osearch.check_topk(s.cpu().numpy(), r.cpu().numpy(), ref_s, ref_r,
+                               lambda qi, rr: rows64[rr] @ q64[qi], tol=1e-5, tie_band=2e-6)
+    assert not probs, probs[:5]
+
+
+def test_rerank_lifts_recall(rivf):
+    from rfx.index import DeviceIndex
+    dim, nlist, n = 768, 64, 30000
+    rows = rivf.synth_clustered(7, 64, 5, 0, n, dim, "bf16")
+    ix = rivf.IvfIndex(dim, nlist)
+    ix.train(rows[::4].contiguous(), iters=6)
+    ix.add(rows)
+    bf = DeviceIndex(dim, "bf16")
+    bf.add(rows)
+    q = rivf.synth_clustered(7, 64, 81, 0, 200, dim, "bf16")
+    _, r_bf = bf.search(q, 10)
+    _, r_ivf = ix.search(q, 10, 8)
+    _, r_rr = ix.search_rerank(q, 10, 8, rows)
+    r_bf, r_ivf, r_rr = r_bf.cpu().numpy(), r_ivf.cpu().numpy(), r_rr.cpu().numpy()
+    rec = lambda r: np.mean([len(set(r[i]) & set(r_bf[i])) / 10 for i in range(len(r_bf))])
+    assert rec(r_rr) >= rec(r_ivf) and rec(r_rr) >= 0.97, (rec(r_ivf), rec(r_rr))
