@@ -199,6 +199,9 @@ int rfx_ivf_set_centroids(rfx_ivf_t h, const int8_t* centroids_d /* [nlist][dim]
 int rfx_ivf_get_centroids(rfx_ivf_t h, int8_t* centroids_d, float* factors_d, void* stream);
 int rfx_ivf_add(rfx_ivf_t h, const void* rows_d, int64_t n, int dtype, void* stream);
 int rfx_ivf_build(rfx_ivf_t h, void* stream);
+/* Persist / restore (like rfx_index_save/load): centroids, per-row codes, scales and labels. */
+int rfx_ivf_save(rfx_ivf_t h, const char* path);
+int rfx_ivf_load(const char* path, int device, rfx_ivf_t* out);
 /* inspection (tests): per-row codes / scales / list labels in insertion order; list offsets
  * [nlist+1] and row ids in list order */
 int rfx_ivf_codes(rfx_ivf_t h, int8_t* codes_d, float* inv_d, int32_t* labels_d, void* stream);

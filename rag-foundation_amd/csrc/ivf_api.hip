@@ -7,7 +7,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <string>
 #include <atomic>
 #include <map>
 #include <memory>
@@ -171,6 +174,31 @@ int ivf_layout(const Ivf& iv, int64_t nq, int k, int nprobe, IvfLayout& L) {
   L.cr = o, o += al256((size_t)nq * L.ncand * 4);
   L.total = o;
   return RFX_OK;
+}
+
+
+// chunked device <-> file copies (persistence)
+bool write_dev(FILE* f, const void* d, size_t n) {
+  std::vector<uint8_t> buf;
+  const size_t chunk = (size_t)256 << 20;
+  for (size_t off = 0; off < n; off += chunk) {
+    const size_t nb = std::min(chunk, n - off);
+    buf.resize(nb);
+    if (hipMemcpy(buf.data(), (const uint8_t*)d + off, nb, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    if (fwrite(buf.data(), 1, nb, f) != nb) return false;
+  }
+  return true;
+}
+bool read_dev(FILE* f, void* d, size_t n) {
+  std::vector<uint8_t> buf;
+  const size_t chunk = (size_t)256 << 20;
+  for (size_t off = 0; off < n; off += chunk) {
+    const size_t nb = std::min(chunk, n - off);
+    buf.resize(nb);
+    if (fread(buf.data(), 1, nb, f) != nb) return false;
+    if (hipMemcpy((uint8_t*)d + off, buf.data(), nb, hipMemcpyHostToDevice) != hipSuccess) return false;
+  }
+  return true;
 }
 
 }  // namespace
@@ -455,6 +483,71 @@ int rfx_ivf_search_rerank(rfx_ivf_t h, const void* queries_d, int64_t nq, int dt
   if (rfx::launch_topk_merge(rs, rr, 1, nq, rerank_k, k, 0, out_scores_d, out_rows_d, st))
     return api_fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
   IVF_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
+// Persistence: "RFXIVF01", {version 1, dim, nlist, trained}, rows, then the int8 centroids and
+// the per-row codes / scales / labels in insertion order.  Factors and posting lists are derived
+// (recomputed on load).  Written to path.tmp, then renamed.
+int rfx_ivf_save(rfx_ivf_t h, const char* path) {
+  auto iv = get(h);
+  if (!iv || !path) return api_fail(RFX_EINVAL, "unknown IVF handle / null path");
+  std::lock_guard<std::mutex> lk(iv->mu);
+  IVF_HIP(hipSetDevice(iv->device));
+  IVF_HIP(hipDeviceSynchronize());
+  const std::string tmp = std::string(path) + ".tmp";
+  FILE* f = fopen(tmp.c_str(), "wb");
+  if (!f) return api_fail(RFX_EIO, "cannot open %s", tmp.c_str());
+  const uint32_t hdr[4] = {1u, (uint32_t)iv->dim, (uint32_t)iv->nlist, (uint32_t)iv->trained};
+  const int64_t rows = iv->rows;
+  bool ok = fwrite("RFXIVF01", 1, 8, f) == 8 && fwrite(hdr, 4, 4, f) == 4 && fwrite(&rows, 8, 1, f) == 1;
+  ok = ok && write_dev(f, iv->qc, (size_t)iv->nlist * iv->dim);
+  if (rows > 0) {
+    ok = ok && write_dev(f, iv->codes, (size_t)rows * iv->dim) && write_dev(f, iv->inv, (size_t)rows * 4) &&
+         write_dev(f, iv->labels, (size_t)rows * 4);
+  }
+  ok = (fclose(f) == 0) && ok;
+  if (!ok) return api_fail(RFX_EIO, "write failed for %s", tmp.c_str());
+  if (rename(tmp.c_str(), path) != 0) return api_fail(RFX_EIO, "rename to %s failed", path);
+  return RFX_OK;
+}
+
+int rfx_ivf_load(const char* path, int device, rfx_ivf_t* out) {
+  if (!path || !out) return api_fail(RFX_EINVAL, "null path / out");
+  FILE* f = fopen(path, "rb");
+  if (!f) return api_fail(RFX_EIO, "cannot open %s", path);
+  char magic[8];
+  uint32_t hdr[4];
+  int64_t rows = 0;
+  if (fread(magic, 1, 8, f) != 8 || memcmp(magic, "RFXIVF01", 8) != 0 || fread(hdr, 4, 4, f) != 4 ||
+      fread(&rows, 8, 1, f) != 1 || hdr[0] != 1u || rows < 0) {
+    fclose(f);
+    return api_fail(RFX_EIO, "%s is not an rfx IVF file", path);
+  }
+  rfx_ivf_t h = 0;
+  int rc = rfx_ivf_create(device, (int)hdr[1], (int)hdr[2], &h);
+  if (rc) {
+    fclose(f);
+    return rc;
+  }
+  auto iv = get(h);
+  bool ok = read_dev(f, iv->qc, (size_t)iv->nlist * iv->dim);
+  if (ok && rows > 0) {
+    rc = grow_rows(*iv, rows, nullptr);
+    ok = rc == RFX_OK && read_dev(f, iv->codes, (size_t)rows * iv->dim) && read_dev(f, iv->inv, (size_t)rows * 4) &&
+         read_dev(f, iv->labels, (size_t)rows * 4);
+  }
+  fclose(f);
+  if (!ok) {
+    rfx_ivf_destroy(h);
+    return rc ? rc : api_fail(RFX_EIO, "truncated IVF file %s", path);
+  }
+  iv->rows = rows;
+  iv->trained = hdr[3] != 0;
+  iv->dirty = true;
+  rfx::ivf::launch_centroid_update(nullptr, nullptr, iv->nlist, iv->dim, iv->qc, iv->fc, nullptr);
+  IVF_HIP(hipDeviceSynchronize());
+  *out = h;
   return RFX_OK;
 }
 

@@ -89,6 +89,8 @@ SIGNATURES = {
     "rfx_ivf_get_centroids": ([_u64, _p, _p, _p], _i),
     "rfx_ivf_add": ([_u64, _p, _i64, _i, _p], _i),
     "rfx_ivf_build": ([_u64, _p], _i),
+    "rfx_ivf_save": ([_u64, _cs], _i),
+    "rfx_ivf_load": ([_cs, _i, _pu64], _i),
     "rfx_ivf_codes": ([_u64, _p, _p, _p, _p], _i),
     "rfx_ivf_lists": ([_u64, _p, _p, _p], _i),
     "rfx_ivf_search_workspace_bytes": ([_u64, _i64, _i, _i, _psz], _i),

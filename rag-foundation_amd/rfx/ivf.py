@@ -16,12 +16,27 @@ from ._lib import check, lib, ptr, stream_ptr
 
 
 class IvfIndex:
-    def __init__(self, dim: int, nlist: int, device: int = 0):
+    def __init__(self, dim: int, nlist: int, device: int = 0, _handle=None):
         self.dim, self.nlist, self.device = int(dim), int(nlist), int(device)
+        if _handle is not None:
+            self.handle = _handle
+            return
         h = ctypes.c_uint64()
         with torch.cuda.device(self.device):
             check(lib.rfx_ivf_create(self.device, self.dim, self.nlist, ctypes.byref(h)))
         self.handle = h.value
+
+    def save(self, path: str) -> None:
+        check(lib.rfx_ivf_save(self.handle, path.encode()))
+
+    @classmethod
+    def load(cls, path: str, device: int = 0) -> "IvfIndex":
+        h = ctypes.c_uint64()
+        with torch.cuda.device(device):
+            check(lib.rfx_ivf_load(path.encode(), int(device), ctypes.byref(h)))
+        dim, nlist = ctypes.c_int(), ctypes.c_int()
+        check(lib.rfx_ivf_info(h.value, ctypes.byref(dim), ctypes.byref(nlist), None, None))
+        return cls(dim.value, nlist.value, device, _handle=h.value)
 
     def close(self) -> None:
         if getattr(self, "handle", None):

@@ -204,3 +204,19 @@ def test_rerank_lifts_recall(rivf):
     r_bf, r_ivf, r_rr = r_bf.cpu().numpy(), r_ivf.cpu().numpy(), r_rr.cpu().numpy()
     rec = lambda r: np.mean([len(set(r[i]) & set(r_bf[i])) / 10 for i in range(len(r_bf))])
     assert rec(r_rr) >= rec(r_ivf) and rec(r_rr) >= 0.97, (rec(r_ivf), rec(r_rr))
+
+
+def test_save_load_roundtrip(rivf, tmp_path):
+    ix, rows, codes, inv, qc, fc = build(rivf, 5000, 256, 32)
+    q = rivf.synth_clustered(7, 48, 92, 0, 40, 256, "bf16")
+    s1, r1 = ix.search(q, 10, 6)
+    path = str(tmp_path / "ivf.rfx")
+    ix.save(path)
+    ix2 = rivf.IvfIndex.load(path)
+    assert ix2.rows == ix.rows and ix2.trained and ix2.nlist == 32
+    s2, r2 = ix2.search(q, 10, 6)
+    assert torch.equal(r1, r2) and torch.equal(s1, s2)
+    assert torch.equal(ix2.centroids()[1], ix.centroids()[1])
+    with pytest.raises(RuntimeError):
+        (tmp_path / "bad.rfx").write_bytes(b"RFXIDX01garbage")
+        rivf.IvfIndex.load(str(tmp_path / "bad.rfx"))
