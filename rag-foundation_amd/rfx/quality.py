@@ -1,0 +1,37 @@
+"""Retrieval quality metrics for regression runs ("extend scripts/benchmark
+citation_hit (metrics.py:73-92) to recall@k against oracle rows").
+
+citation_recall_at_k keeps the reference's matching rule — case-insensitive equality of a
+citation's doc_id / sourceId / uri / title against the gold document ids (metrics.py:73-92) — but
+reports the FRACTION of gold documents cited within the first k citations instead of a 0/1 hit.
+recall_at_k compares retrieved row ids with the exact (oracle / brute-force) top-k rows.
+"""
+from typing import Iterable, Optional, Sequence
+
+
+def _cite_key(c: dict) -> str:
+    return str(c.get("doc_id") or c.get("sourceId") or c.get("uri") or c.get("title") or "").lower()
+
+
+def citation_recall_at_k(citations: Iterable[dict], gold_doc_ids: Sequence[str], k: int) -> Optional[float]:
+    """None without gold ids (as citation_hit); else |gold ∩ first-k citations| / |gold|."""
+    if not gold_doc_ids:
+        return None
+    gold = {str(g).lower() for g in gold_doc_ids}
+    seen = {_cite_key(c) for c in list(citations or [])[:k]}
+    return len(gold & seen) / len(gold)
+
+
+def recall_at_k(retrieved: Sequence[Sequence[int]], truth: Sequence[Sequence[int]], k: int) -> float:
+    """Mean over queries of |retrieved[:k] ∩ truth[:k]| / |truth[:k]| (rows < 0 = padding, ignored)."""
+    if len(retrieved) != len(truth):
+        raise ValueError("retrieved and truth must have one row list per query")
+    tot, n = 0.0, 0
+    for got, ref in zip(retrieved, truth):
+        ref_k = {int(r) for r in list(ref)[:k] if int(r) >= 0}
+        if not ref_k:
+            continue
+        got_k = {int(r) for r in list(got)[:k] if int(r) >= 0}
+        tot += len(got_k & ref_k) / len(ref_k)
+        n += 1
+    return tot / n if n else 1.0
