@@ -42,6 +42,11 @@ def parse():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-sample-rows", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # rehearsal of the multi-GPU path on a one-GPU box: gloo transport, every rank on cuda:0,
+    # and --check compares the sharded result with a whole-index search on rank 0
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--one-device", action="store_true")
+    ap.add_argument("--check", action="store_true")
     return ap.parse_args()
 
 
@@ -73,9 +78,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if a.one_device:
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     from rfx import dist as rdist
     from rfx.index import DeviceIndex, synth_rows, topk_merge, topk_merge_records
@@ -125,9 +135,19 @@ def main():
     elapsed = time.perf_counter() - t0
     scan_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
     if world > 1:
-        t = torch.tensor([elapsed, scan_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, scan_ms], dtype=torch.float64, device=dev if a.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, scan_ms = float(t[0]), float(t[1])
+    if a.check:  # the global top-k of the last step equals one whole-index search (exact)
+        got_s, got_r = out
+        if rank == 0:
+            full = DeviceIndex(a.dim, a.dtype, local, capacity=a.rows)
+            full.add_synthetic(a.seed, a.rows)
+            ref_s, ref_r = full.search(q, a.k)
+            if not (torch.equal(got_r, ref_r) and torch.equal(got_s, ref_s)):
+                raise SystemExit("--check: sharded result differs from the whole-index search")
+            print("check ok: sharded top-k == whole-index top-k", flush=True)
+            del full
 
     esz = {"bf16": 2, "f16": 2, "f32": 4}[a.dtype]
     # algorithmic bytes of one scan launch on the largest shard: rows read once,
