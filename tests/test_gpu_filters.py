@@ -139,3 +139,29 @@ def test_retriever_filter_end_to_end(rindex, tmp_path):
     assert titles({"tenant": "acme"}) == [t for t in everything if t == "acme.txt"]
     assert titles({"tenant": ["globex"]}) == [t for t in everything if t == "globex.txt"]
     assert titles({"tenant": "initech"}) == []
+
+
+def test_filter_survives_store_reload(rindex, tmp_path):
+    # upload metadata is persisted with the store (manifest.json): another process (a fresh
+    # registry on the same directory, as the API workers load what the ingestion worker wrote)
+    # applies the same filter
+    from rfx.adapter import LocalGpuRag
+    from rfx.retriever import GpuRetriever
+    from rfx.store import StoreRegistry, set_registry
+
+    root = str(tmp_path / "stores")
+    set_registry(StoreRegistry(root=root))
+    rag = LocalGpuRag(GpuRetriever(dtype="bf16"), top_k=5)
+    st = rag.create_store("tenants")
+    for tenant, words in (("acme", "alpha beta gamma delta " * 8), ("globex", "alpha beta epsilon zeta " * 8)):
+        p = tmp_path / f"{tenant}.txt"
+        p.write_text(words)
+        rag.upload_file(st, str(p), display_name=f"{tenant}.txt",
+                        custom_metadata=[{"key": "tenant", "string_value": tenant}],
+                        chunking_config={"white_space_config": {"max_tokens_per_chunk": 4, "max_overlap_tokens": 0}})
+    ask = lambda r: [c["title"] for c in r.extract_citations_from_response(
+        r.ask(contents="alpha beta", store_names=[st], metadata_filter={"tenant": "globex"}, model="m", top_k=20))]
+    before = ask(rag)
+    set_registry(StoreRegistry(root=root))  # fresh process view: loads manifest + index from disk
+    after = ask(LocalGpuRag(GpuRetriever(dtype="bf16"), top_k=5))
+    assert before == after and set(after) == {"globex.txt"}
