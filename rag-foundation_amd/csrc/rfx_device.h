@@ -97,10 +97,19 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// lane l receives lane l-1's value (lane 0 keeps its own): one DPP move (wave_shr:1, GFX9 DPP)
+// instead of a ds_bpermute round trip through the LDS crossbar — the list insert's critical path.
+__device__ __forceinline__ int lane_shr1(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xf, 0xf, false); }
+__device__ __forceinline__ float lane_shr1(float v) { return __int_as_float(lane_shr1(__float_as_int(v))); }
+__device__ __forceinline__ long long lane_shr1(long long v) {
+  const int lo = lane_shr1((int)v), hi = lane_shr1((int)(v >> 32));
+  return (long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
 // ---- wave-resident top-K list ------------------------------------------------------------------
 // The list lives in lanes 0..K-1 of (ls, lr), best first; empty slots are (-inf, kEmptyRow).
 // Candidates arrive one per lane; those that beat the wave-uniform threshold (entry K-1) are
-// inserted one at a time (ballot + popcount for the position, one shuffle to shift).
+// inserted one at a time (ballot + popcount for the position, one DPP lane shift).
 template <int K>
 struct WaveList {
   float ls;
@@ -126,8 +135,8 @@ struct WaveList {
       if (!better(s, r, ts, tr)) continue;  // wave-uniform: threshold may have risen
       const bool b = (lane < K) && better(ls, lr, s, r);
       const int pos = __popcll(__ballot(b));
-      const float us = __shfl_up(ls, 1);
-      const int ur = __shfl_up(lr, 1);
+      const float us = lane_shr1(ls);
+      const int ur = lane_shr1(lr);
       if (lane > pos && lane < K) {
         ls = us;
         lr = ur;
@@ -149,19 +158,22 @@ struct WaveList64 {
   long long lr;
   float ts;
   long long tr;
+  float fs;  // admission floor (wave-uniform): the threshold never drops below it
+  long long fr;
 
   __device__ __forceinline__ void init() {
     ls = -__builtin_inff();
     lr = 0x7fffffffffffffffll;
-    ts = -__builtin_inff();
-    tr = 0x7fffffffffffffffll;
+    ts = fs = -__builtin_inff();
+    tr = fr = 0x7fffffffffffffffll;
   }
 
-  // empty list whose admission threshold is (s, r): only strictly better candidates enter
+  // empty list whose admission threshold is (s, r): only strictly better candidates enter, also
+  // after inserts (the threshold is max(floor, entry K-1), so an empty tail cannot lower it)
   __device__ __forceinline__ void init_above(float s, long long r) {
     init();
-    ts = s;
-    tr = r;
+    ts = fs = s;
+    tr = fr = r;
   }
 
   __device__ __forceinline__ void offer(float cs, long long cr, bool valid) {
@@ -176,8 +188,8 @@ struct WaveList64 {
       if (!better64(s, r, ts, tr)) continue;
       const bool b = (lane < K) && better64(ls, lr, s, r);
       const int pos = __popcll(__ballot(b));
-      const float us = __shfl_up(ls, 1);
-      const long long ur = __shfl_up(lr, 1);
+      const float us = lane_shr1(ls);
+      const long long ur = lane_shr1(lr);
       if (lane > pos && lane < K) {
         ls = us;
         lr = ur;
@@ -186,9 +198,12 @@ struct WaveList64 {
         ls = s;
         lr = r;
       }
-      ts = readlane_f(ls, K - 1);
-      tr = (long long)(((uint64_t)(uint32_t)readlane_i((int)(lr >> 32), K - 1) << 32) |
-                       (uint32_t)readlane_i((int)lr, K - 1));
+      const float ks = readlane_f(ls, K - 1);
+      const long long kr = (long long)(((uint64_t)(uint32_t)readlane_i((int)(lr >> 32), K - 1) << 32) |
+                                       (uint32_t)readlane_i((int)lr, K - 1));
+      const bool above = better64(ks, kr, fs, fr);
+      ts = above ? ks : fs;
+      tr = above ? kr : fr;
     }
   }
 };

@@ -134,3 +134,34 @@ def test_scan_then_records_then_gathered_equals_search(rindex):
     s, r = rindex.merge_gathered(torch.stack(recs), 10)
     assert torch.equal(r, ref_r)
     assert torch.equal(s, ref_s)
+
+
+@pytest.mark.parametrize("nq,n_lists,L,k", [(1, 391, 16, 10), (1, 3000, 16, 16), (3, 391, 16, 5), (32, 700, 10, 10),
+                                            (7, 130, 16, 10), (1, 129, 16, 10), (2, 5000, 4, 4), (33, 512, 10, 10)])
+@pytest.mark.parametrize("ties", [False, True])
+def test_merge_few_queries_many_lists_matches_oracle(rindex, nq, n_lists, L, k, ties):
+    """Few queries over many candidate lists (config 2's shape: 1 query, 391 lists of 16), where
+    the heads bound does most of the pruning; equal to the oracle for every list_len hint,
+    with empty list tails and tied scores."""
+    rng = np.random.default_rng(nq * 7919 + n_lists * 31 + L + k + ties)
+    s, r = sorted_lists(rng, nq, n_lists, L, 10_000_000, empty_frac=0.2, ties=ties)
+    ref_s, ref_r = oracle_merge(s, r, k)
+    for rows_dtype in (torch.int32, torch.int64):
+        for ll in (L, 1):
+            cs = torch.from_numpy(s.copy()).cuda()
+            cr = torch.from_numpy(r).to(rows_dtype).cuda()
+            out_s, out_r = rindex.topk_merge(cs, cr, k, list_len=ll, row_offset=5)
+            assert np.array_equal(out_r.cpu().numpy(), np.where(ref_r >= 0, ref_r + 5, -1)), (ll, rows_dtype)
+            assert np.array_equal(out_s.cpu().numpy(), ref_s)
+
+
+def test_merge_heads_bound_unsorted_and_all_empty(rindex):
+    rng = np.random.default_rng(11)
+    s = rng.standard_normal((2, 6400)).astype(np.float32)
+    r = np.stack([rng.permutation(10**6)[:6400] for _ in range(2)]).astype(np.int64)
+    s[1] = -np.inf  # query 1: nothing live
+    r[1] = 0x7fffffff
+    ref_s, ref_r = oracle_merge(s, r, 10)
+    cs, cr = torch.from_numpy(s.copy()).cuda(), torch.from_numpy(r).to(torch.int32).cuda()
+    out_s, out_r = rindex.topk_merge(cs, cr, 10, list_len=16)  # wrong hint: unsorted lists
+    assert np.array_equal(out_r.cpu().numpy(), ref_r) and np.array_equal(out_s.cpu().numpy(), ref_s)
