@@ -477,25 +477,9 @@ __global__ __launch_bounds__(512) void merge_kernel(Src src, int list_len, int k
       const bool live = hr >= 0 && hr != kNoRow && (R64 || hr != (long long)kEmptyRow);
       mine = live ? ord_f32(hs) : 0u;
     }
-    hk[tid] = mine;
   }
-  __syncthreads();
-  if (nh >= k_out) {
-    uint32_t cand = 0u;
-    if (mine) {
-      int c = 0;
-      for (int i = 0; i < (nh + 3) / 4; ++i) {
-        const uint4 v = hk4[i];
-        c += (v.x >= mine) + (v.y >= mine) + (v.z >= mine) + (v.w >= mine);
-      }
-      cand = c >= k_out ? mine : 0u;
-    }
-#pragma unroll
-    for (int off = 32; off; off >>= 1) cand = max(cand, (uint32_t)__shfl_xor((int)cand, off));
-    if (lane == 0 && cand) atomicMax(&tb, cand);
-  }
+  uint32_t m = 0u;  // list bound (below), reduced after the barrier
   if (list_len > 1 && list_len >= k_out) {
-    uint32_t m = 0u;
     for (int64_t j = tid; j < n / list_len; j += 512) {
       uint32_t mj = 0xffffffffu;  // min over the list's first k_out entries (sorted or not)
       for (int e0 = 0; e0 < k_out; e0 += 8) {  // 8 independent loads in flight per round
@@ -517,8 +501,24 @@ __global__ __launch_bounds__(512) void merge_kernel(Src src, int list_len, int k
     }
 #pragma unroll
     for (int off = 32; off; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
-    if (lane == 0) atomicMax(&tb, m);
   }
+  if (tid < 512) hk[tid] = mine;  // after the list pass, so its loads overlap the head load
+  __syncthreads();
+  if (nh >= k_out) {
+    uint32_t cand = 0u;
+    if (mine) {
+      int c = 0;
+      for (int i = 0; i < (nh + 3) / 4; ++i) {
+        const uint4 v = hk4[i];
+        c += (v.x >= mine) + (v.y >= mine) + (v.z >= mine) + (v.w >= mine);
+      }
+      cand = c >= k_out ? mine : 0u;
+    }
+#pragma unroll
+    for (int off = 32; off; off >>= 1) cand = max(cand, (uint32_t)__shfl_xor((int)cand, off));
+    if (lane == 0 && cand) atomicMax(&tb, cand);
+  }
+  if (lane == 0 && m) atomicMax(&tb, m);
   __syncthreads();
   if (tb) {
     const uint32_t u = tb & 0x80000000u ? tb & 0x7fffffffu : ~tb;  // inverse of ord_f32
