@@ -267,8 +267,13 @@ ValuPlan plan_scan_valu(int64_t nrows, int D, int dtype, int64_t nq, int k) {
   p.q_slices = (int)((nq + p.nqt - 1) / p.nqt);
   const int64_t target_waves = 4096;
   int64_t rpw = (nrows + target_waves - 1) / target_waves;
+  static const int rpw_env = [] {  // RFX_VALU_RPW: ablation override of rows per wave
+    const char* e = getenv("RFX_VALU_RPW");
+    return e ? atoi(e) : 0;
+  }();
   if (rpw < 64) rpw = 64;
   rpw = (rpw + 63) / 64 * 64;
+  if (rpw_env >= 4) rpw = rpw_env / 4 * 4;
   int64_t waves = (nrows + rpw - 1) / rpw;
   if (waves < 1) waves = 1;
   p.rows_per_wave = (int)rpw;
