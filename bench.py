@@ -41,13 +41,32 @@ def parse():
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-sample-rows", type=int, default=1_000_000)
+    # corpus copies the steps rotate through: a corpus smaller than the 256 MB Infinity Cache
+    # would otherwise be re-read from the cache (config 2: 307 MB); 0 = enough copies that
+    # ~768 MB of other rows pass between two reads of one copy
+    ap.add_argument("--copies", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # oracle check of the last timed step (rank 0, N = 1): every `stride`-th query against
+    # oracle.search.topk_blocks over ALL rows (read back after the timed region); 0 = off
+    ap.add_argument("--oracle-stride", type=int, default=4)
     # rehearsal of the multi-GPU path on a one-GPU box: gloo transport, every rank on cuda:0,
     # and --check compares the sharded result with a whole-index search on rank 0
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
     ap.add_argument("--one-device", action="store_true")
     ap.add_argument("--check", action="store_true")
     return ap.parse_args()
+
+
+def workload_name(a):
+    """BASELINE.json config this shape is (configs[1..3]); anything else is a custom shape."""
+    shape = (a.rows, a.dim, a.dtype, a.nq, a.k)
+    if shape == (10_000_000, 768, "bf16", 256, 10):
+        return "cfg3"
+    if shape == (100_000, 768, "f32", 1, 10):
+        return "cfg2"
+    if shape[1:] == (1024, "f16", 256, 10) and a.rows in (12_500_000, 100_000_000):
+        return "cfg4" + (" (one GPU's shard)" if a.rows == 12_500_000 else "")
+    return "custom"
 
 
 def cpu_model():
@@ -93,8 +112,16 @@ def main():
     dev = torch.device("cuda", local)
     r0, r1 = rdist.shard_range(a.rows, rank, world)
     n_local = r1 - r0
-    ix = DeviceIndex(a.dim, a.dtype, local, capacity=n_local)
-    ix.add_synthetic(a.seed, n_local, gen_row0=r0)
+    esz = {"bf16": 2, "f16": 2, "f32": 4}[a.dtype]
+    copies = a.copies or min(8, max(1, -(-(768 << 20) // max(n_local * a.dim * esz, 1)) + 1))
+    if copies > 1 and n_local * a.dim * esz > (1 << 30):
+        copies = 1  # far beyond the Infinity Cache already
+    ixs = []
+    for _ in range(copies):
+        c = DeviceIndex(a.dim, a.dtype, local, capacity=n_local)
+        c.add_synthetic(a.seed, n_local, gen_row0=r0)
+        ixs.append(c)
+    ix = ixs[0]
     q = synth_rows(a.seed + 1, 0, a.nq, a.dim, a.dtype, local)
     kern, n_cand = ix.plan(a.nq, a.k)
     list_len = ix.list_len(a.nq, a.k)  # sorted candidate lists: the merge bounds by their k-th entries
@@ -105,12 +132,14 @@ def main():
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize()
 
+    from rfx import _lib
     from rfx._lib import check, lib, ptr, stream_ptr
 
-    def step(ev=None):
+    def step(i, ev=None):
+        h = ixs[i % copies].handle
         if ev is not None:
             ev[0].record(stream)
-        check(lib.rfx_scan_topk(ix.handle, ptr(q), a.nq, a.k, ptr(cs), ptr(cr), ptr(ws), ws.numel(),
+        check(lib.rfx_scan_topk(h, ptr(q), a.nq, a.k, ptr(cs), ptr(cr), ptr(ws), ws.numel(),
                                 stream_ptr(stream)))
         if ev is not None:
             ev[1].record(stream)
@@ -120,15 +149,15 @@ def main():
         topk_merge_records(cs, cr, a.k, row_offset=r0, stream=stream, list_len=list_len, out=rec)
         return rdist.gather_merge_records(rec, a.k, stream=stream)
 
-    for _ in range(a.warmup):
-        step()
+    for i in range(a.warmup):
+        step(i)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        out = step(evs[i])
+        out = step(i, evs[i])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -149,7 +178,6 @@ def main():
             print("check ok: sharded top-k == whole-index top-k", flush=True)
             del full
 
-    esz = {"bf16": 2, "f16": 2, "f32": 4}[a.dtype]
     # algorithmic bytes of one scan launch on the largest shard: rows read once,
     # queries read once, (score,row) results written once.
     n_max = rdist.shard_range(a.rows, 0, world)[1]
@@ -170,12 +198,14 @@ def main():
         "vs_baseline": None,
         "dtype": a.dtype,
         "data": "synthetic (splitmix64 counter-based corpus + queries, rows L2-normalised; oracle/synth.py)",
-        "config": {"workload": f"cfg3: {a.rows}x{a.dim} {a.dtype} corpus row-sharded over {world} GPU(s), "
-                               f"{a.nq} queries/batch, brute-force top-{a.k}",
+        "config": {"workload": f"{workload_name(a)}: {a.rows}x{a.dim} {a.dtype} corpus row-sharded over {world} "
+                               f"GPU(s), {a.nq} queries/batch, brute-force top-{a.k}",
                    "rows": a.rows, "dim": a.dim, "nq": a.nq, "k": a.k, "parallelism": f"rowshard{world}",
+                   "corpus_copies": copies,
                    "scan_kernel": {0: "valu", 1: "mfma128", 2: "mfma256", 3: "mfma_qstationary128",
                                    4: "mfma_qstationary256", 5: "mfma_qstationary256_2wps"}[kern]},
         "achieved_hbm_gbps_per_gpu": round(achieved, 1),
+        "build_id": _lib.BUILD_ID,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": load_pmc_traffic(workload_key),
                      "kernel": {0: "scan_valu_kernel", 1: "scan_mfma_kernel", 2: "scan_mfma2_kernel", 3: "scan_mfma3_kernel",
@@ -183,12 +213,50 @@ def main():
                      "kernel_ms": round(scan_ms, 4), "alg_bytes_per_launch": alg_bytes},
     }
 
+    check_ok = True
+    if rank == 0 and world == 1 and a.oracle_stride > 0:
+        result["oracle_check"] = oracle_check(ix, q, out, a)
+        check_ok = result["oracle_check"]["ok"]
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(ix, q, a)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if not check_ok:
+        raise SystemExit("oracle check of the last timed step FAILED (see oracle_check in the JSON line)")
+
+
+def oracle_check(ix, q, out, a):
+    """Checker (not timed): the last timed step's top-k for every a.oracle_stride-th query against
+    the CPU oracle over ALL rows of the corpus, read back from HBM 1M rows at a time and widened
+    exactly to f32 on the host (oracle.search.topk_blocks: f32 screen with a rigorous rounding
+    bound + exact rescoring).  Parity rule: oracle.search.check_topk (1e-5 / 2e-6)."""
+    import numpy as np
+
+    from oracle import search as osearch
+
+    t0 = time.perf_counter()
+    sel = list(range(0, a.nq, a.oracle_stride))
+    q64 = q[sel].cpu().float().numpy().astype(np.float64)
+    blk = 1 << 20
+
+    def blocks():
+        for r0 in range(0, ix.rows, blk):
+            yield r0, ix.read(r0, min(blk, ix.rows - r0)).cpu().float().numpy()
+
+    ref_s, ref_r = osearch.topk_blocks(q64, blocks(), a.k)
+    got_s, got_r = out[0][sel].cpu().numpy(), out[1][sel].cpu().numpy()
+
+    def scores_of(qi, rows):
+        return np.array([ix.read(int(x), 1).cpu().float().numpy()[0].astype(np.float64) @ q64[qi] for x in rows])
+
+    probs = osearch.check_topk(got_s, got_r, ref_s, ref_r, scores_of, tol=1e-5, tie_band=2e-6)
+    same = got_r == ref_r
+    err = float(np.abs(got_s[same].astype(np.float64) - ref_s[same]).max()) if same.any() else 0.0
+    return {"ok": not probs, "queries": len(sel), "rows": ix.rows, "problems": probs[:3],
+            "rows_identical_frac": round(float(same.mean()), 6), "max_abs_score_err": err,
+            "rule": "oracle.search.check_topk tol 1e-5, tie band 2e-6", "secs": round(time.perf_counter() - t0, 1)}
 
 
 def cpu_baseline(ix, q, a):

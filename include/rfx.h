@@ -55,6 +55,9 @@ typedef uint64_t rfx_index_t;
 const char* rfx_last_error(void);
 /* ABI version (major*10000 + minor*100 + patch). */
 int rfx_version(void);
+/* 16-hex sha256 of the sources the library was built from (csrc/Makefile); the Python host
+ * recomputes it from the tree and refuses a stale library (rfx/_lib.py). */
+const char* rfx_build_id(void);
 /* Number of visible HIP devices. */
 int rfx_device_count(int* out_n);
 /* Bind the calling thread to a device (process-level singleton per device).

@@ -26,26 +26,26 @@
 // multiple of 128, so the ragged last tile needs no clamping or masking.
 // Algorithmic bytes per tile: 32 * D * esize.
 #pragma once
-#include "k_scan_mfma4.h"
+#include "k_mfma_common.h"
 
 namespace rfx {
 namespace k5 {
 
-using k4::batomic_umax;
-using k4::bdma;
-using k4::bdma_nt;
-using k4::bdma_sc1;
-using k4::fold;
-using k4::make_rsrc;
-using k4::v4i32;
-using k4::glds;
-using k4::glds_sc1;
-using k4::mfma;
-using k4::mfma16;
-using k4::v4f32x4;
-using k4::tau_min;
-using k4::unord;
-using k4::v4f32x16;
+using mfc::batomic_umax;
+using mfc::bdma;
+using mfc::bdma_nt;
+using mfc::bdma_sc1;
+using mfc::fold;
+using mfc::make_rsrc;
+using mfc::v4i32;
+using mfc::glds;
+using mfc::glds_sc1;
+using mfc::mfma;
+using mfc::mfma16;
+using mfc::v4f32x4;
+using mfc::tau_min;
+using mfc::unord;
+using mfc::v4f32x16;
 
 // 16 values of four 16x16 accumulators as one flat vector (no copies)
 struct Acc4View {

@@ -140,10 +140,8 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
   if (L.kernel) {
     L.n_cand = L.mp.n_lists * L.mp.k_lane;
     L.q_bytes = (size_t)L.mp.nq_pad * ix.dim * 2;
-    if (L.kernel == 5)  // (>= the kernel-4 table: the debug path may run either on this layout)
-      tau_bytes = std::max(rfx::tau_bytes_mfma5(L.mp), rfx::tau_bytes_mfma4(L.mp));
-    else if (L.kernel == 4)
-      tau_bytes = rfx::tau_bytes_mfma4(L.mp);
+    if (L.kernel == 5)
+      tau_bytes = rfx::tau_bytes_mfma5(L.mp);
     else if (L.kernel >= 2)
       tau_bytes = (size_t)(L.mp.nq_pad + 256) * 4;  // + slack: 1 KB threshold DMA per group
   } else {
@@ -169,14 +167,12 @@ size_t scan_ws_bytes(const SearchLayout& L) { return L.cs_off; }
 int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq, float* cs, int32_t* cr,
               uint8_t* ws, hipStream_t st, const uint32_t* mask = nullptr) {
   if (ix.rows == 0 || nq == 0) return RFX_OK;
-  if (mask && L.kernel == 4) return fail(RFX_EUNSUPPORTED, "kernel 4 (ablation only) has no row-mask variant");
   if (L.kernel >= 1) {
     void* qpad = ws + L.q_off;
     rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, 2, qpad, st);
     uint32_t* tau = (uint32_t*)(ws + L.tau_off);
     const int rc =
         L.kernel == 5 ? rfx::launch_scan_mfma5(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
-        : L.kernel == 4 ? rfx::launch_scan_mfma4(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st)
         : L.kernel == 3 ? rfx::launch_scan_mfma3(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
         : L.kernel == 2 ? rfx::launch_scan_mfma2(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
                         : rfx::launch_scan_mfma(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, cs, cr, st, mask);
@@ -576,6 +572,8 @@ int rfx_merge_gathered(const void* records_d, int world, int64_t nq, int k, floa
   return RFX_OK;
 }
 
+#ifdef RFX_DEBUG_BUILD
+// ---- debug build only (librfx_dbg.so, `make dbg`; tools/) ------------------------------------
 // Diagnostic entry point (not in include/rfx.h): the bf16 / nq 256 / k 10 MFMA scan with
 // parts of the kernel removed, for profiling (mode 1 = no top-k epilogue, 2 = no MFMA).
 int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k, int mode, float* cs, int32_t* cr,
@@ -620,6 +618,8 @@ int rfx_dbg_stream_read(rfx_index_t h, void* scratch4_d, void* stream) {
   RFX_HIP(hipGetLastError());
   return RFX_OK;
 }
+
+#endif  // RFX_DEBUG_BUILD
 
 int rfx_search(rfx_index_t h, const void* queries_d, int64_t nq, int k, float* out_scores_d, int64_t* out_rows_d,
                void* ws_d, size_t ws_bytes, void* stream) {

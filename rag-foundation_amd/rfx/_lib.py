@@ -7,6 +7,7 @@ runtime per process, and device pointers / streams from torch are valid inside t
 There is NO fallback: if librfx.so is missing or fails to load, importing this module raises.
 """
 import ctypes
+import hashlib
 import os
 
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
@@ -46,6 +47,33 @@ if not os.path.exists(LIB_PATH):
                       f"(make -C rag-foundation_amd/csrc); there is no CPU fallback")
 
 lib = ctypes.CDLL(LIB_PATH)
+CSRC = os.path.join(os.path.dirname(_HERE), "csrc")
+
+
+def source_hash() -> str:
+    """sha256 (16 hex) of the library sources, computed exactly as csrc/Makefile does for the
+    rfx_build_id() it bakes into librfx.so: *.hip *.h *.cpp in byte order, then the Makefile
+    and include/rfx.h.  None when the sources are not shipped next to the library."""
+    try:
+        names = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".h", ".cpp")))
+        paths = [os.path.join(CSRC, f) for f in names] + [os.path.join(CSRC, "Makefile"),
+                                                           os.path.join(CSRC, "..", "..", "include", "rfx.h")]
+        h = hashlib.sha256()
+        for q in paths:
+            with open(q, "rb") as f:
+                h.update(f.read())
+        return h.hexdigest()[:16]
+    except OSError:
+        return None
+
+
+lib.rfx_build_id.argtypes = []
+lib.rfx_build_id.restype = ctypes.c_char_p
+BUILD_ID = lib.rfx_build_id().decode()
+SOURCE_HASH = source_hash()
+if SOURCE_HASH is not None and SOURCE_HASH != BUILD_ID and os.environ.get("RFX_ALLOW_STALE_LIB") != "1":
+    raise ImportError(f"{LIB_PATH} was built from other sources (build id {BUILD_ID}, tree {SOURCE_HASH}): "
+                      f"rebuild with __graft_entry__.build()")
 
 _i = ctypes.c_int
 _i64 = ctypes.c_int64
@@ -62,6 +90,7 @@ _cs = ctypes.c_char_p
 SIGNATURES = {
     "rfx_last_error": ([], ctypes.c_char_p),
     "rfx_version": ([], _i),
+    "rfx_build_id": ([], ctypes.c_char_p),
     "rfx_device_count": ([_pi], _i),
     "rfx_init": ([_i], _i),
     "rfx_index_create": ([_i, _i, _i, _i64, _pu64], _i),

@@ -1,0 +1,86 @@
+"""GPU parity at the sizes the bench times (BASELINE.json configs[2] and configs[3]).
+
+  cfg3: 10M x 768 bf16, nq 256, k 10 -> the headline kernel (plan 5); ALL 256 queries against the
+        CPU oracle over all 10M rows (oracle.search.topk_blocks: exact, block-streamed), and all
+        256 against the VALU kernel (an independent scan), 8 queries per launch.
+  cfg4: one GPU's shard of the 8-GPU config, 12.5M x 1024 f16, nq 256, k 10 (plan 3), ALL 256
+        queries against the oracle over all 12.5M rows.
+Rows come back from the device 1M at a time and are widened to f32 on the host (exact for
+bf16/f16); the oracle screens in f32 with a rigorous rounding bound and rescores the survivors
+exactly.  Parity rule: oracle.search.check_topk (indices exact outside the 2e-6 tie band, scores
+within 1e-5).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import search as osearch
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+TIE = 2e-6
+BLOCK = 1 << 20
+
+
+def host_f32(t: torch.Tensor) -> np.ndarray:
+    return t.cpu().float().numpy()  # bf16/f16 -> f32 widening is exact
+
+
+def device_blocks(ix, n):
+    for r0 in range(0, n, BLOCK):
+        print(f"  oracle block {r0 // BLOCK + 1}/{-(-n // BLOCK)}", flush=True)  # progress (run with -s)
+        yield r0, host_f32(ix.read(r0, min(BLOCK, n - r0)))
+
+
+def oracle_check(ix, n, q, s, r, k):
+    q64 = host_f32(q).astype(np.float64)
+    ref_s, ref_r = osearch.topk_blocks(q64, device_blocks(ix, n), k)
+
+    def scores_of(qi, rows):
+        return np.array([host_f32(ix.read(int(x), 1))[0].astype(np.float64) @ q64[qi] for x in rows])
+
+    probs = osearch.check_topk(s.cpu().numpy(), r.cpu().numpy(), ref_s, ref_r, scores_of, tol=TOL, tie_band=TIE)
+    assert not probs, probs[:5]
+    return ref_s, ref_r
+
+
+@pytest.fixture(scope="module")
+def rindex():
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    import rfx.index as ri
+    return ri
+
+
+def test_cfg3_fullsize_headline_kernel(rindex):
+    n, nq, k = 10_000_000, 256, 10
+    ix = rindex.DeviceIndex(768, "bf16", 0, capacity=n)
+    ix.add_synthetic(0, n)  # bench.py's corpus (seed 0) and queries (seed 1)
+    q = rindex.synth_rows(1, 0, nq, 768, "bf16")
+    assert ix.plan(nq, k)[0] == 5, "cfg3 must run the headline kernel"
+    s, r = ix.search(q, k)
+    torch.cuda.synchronize()
+    oracle_check(ix, n, q, s, r, k)
+    # an independent kernel over the same rows: the VALU scan, 8 queries per launch
+    parts = [ix.search(q[i:i + 8], k) for i in range(0, nq, 8)]
+    assert ix.plan(8, k)[0] == 0
+    s2 = torch.cat([p[0] for p in parts]).cpu().numpy()
+    r2 = torch.cat([p[1] for p in parts]).cpu().numpy()
+    s1, r1 = s.cpu().numpy(), r.cpu().numpy()
+    assert np.abs(s1 - s2).max() <= 2 * TOL
+    for qi, ki in zip(*np.nonzero(r1 != r2)):
+        assert abs(s1[qi, ki] - s2[qi, ki]) <= 2 * TIE
+    ix.close()
+
+
+def test_cfg4_shard_fullsize(rindex):
+    n, nq, k = 12_500_000, 256, 10
+    ix = rindex.DeviceIndex(1024, "f16", 0, capacity=n)
+    ix.add_synthetic(0, n, gen_row0=0)
+    q = rindex.synth_rows(1, 0, nq, 1024, "f16")
+    kern = ix.plan(nq, k)[0]
+    assert kern in (3, 6), kern
+    s, r = ix.search(q, k)
+    torch.cuda.synchronize()
+    oracle_check(ix, n, q, s, r, k)
+    ix.close()
