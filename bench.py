@@ -3,11 +3,13 @@
 Workload (BASELINE.json configs[2], the config the metric is quoted on):
   10M × 768 bf16 corpus (synthetic, counter-based generator, rows L2-normalised), batches of 256
   queries (bf16), brute-force top-10.  With --gpus N the corpus is row-sharded over N ranks
-  (one process per GPU, torch.distributed backend "nccl" = RCCL) and each step ends with the
-  all-gather of per-shard top-k + merge (rfx.dist) — total work fixed => "scaling": "strong".
+  (one process per GPU) and each step ends with the all-gather of per-shard top-k + merge
+  (rfx.dist) — total work fixed => "scaling": "strong".
 A step = one batch: fused MFMA scan + per-shard merge (+ all-gather + global merge for N > 1),
 inputs already resident in HBM.  For N > 1 the shard's top-k goes out as packed records
-(rfx_topk_merge_records), one RCCL all-gather, one HIP merge of the gathered records.
+(rfx_topk_merge_records), one RCCL all-gather issued from inside librfx (rfx_allgather_records on
+an rfx_comm_init_rank communicator), one HIP merge of the gathered records.  torch.distributed
+(gloo) is only the control plane: the RCCL id bootstrap, barriers and the max-over-ranks timing.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--rows R] [--nq Q] [--k K] [--dim D]
                        [--dtype bf16|f16|f32] [--no-cpu-baseline]
@@ -51,7 +53,7 @@ def parse():
     ap.add_argument("--oracle-stride", type=int, default=4)
     # rehearsal of the multi-GPU path on a one-GPU box: gloo transport, every rank on cuda:0,
     # and --check compares the sharded result with a whole-index search on rank 0
-    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"])
+    ap.add_argument("--backend", default="rccl", choices=["rccl", "gloo"])
     ap.add_argument("--one-device", action="store_true")
     ap.add_argument("--check", action="store_true")
     return ap.parse_args()
@@ -99,15 +101,15 @@ def main():
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
     if a.one_device:
         local = 0
+        a.backend = "gloo"  # RCCL refuses two ranks on one GPU: the rehearsal exchanges via the host
     torch.cuda.set_device(local)
     if world > 1:
-        if a.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group("gloo")
+        dist.init_process_group("gloo")  # control plane only (bootstrap, barriers, timing)
 
     from rfx import dist as rdist
     from rfx.index import DeviceIndex, synth_rows, topk_merge, topk_merge_records
+
+    comm = rdist.RcclComm.from_process_group(local) if world > 1 and a.backend == "rccl" else None
 
     dev = torch.device("cuda", local)
     r0, r1 = rdist.shard_range(a.rows, rank, world)
@@ -147,7 +149,7 @@ def main():
             return topk_merge(cs, cr, a.k, row_offset=r0, stream=stream, list_len=list_len)
         # rank-local top-k as all-gather records (global rows), one collective, one HIP merge
         topk_merge_records(cs, cr, a.k, row_offset=r0, stream=stream, list_len=list_len, out=rec)
-        return rdist.gather_merge_records(rec, a.k, stream=stream)
+        return rdist.gather_merge_records(rec, a.k, comm=comm, stream=stream)
 
     for i in range(a.warmup):
         step(i)
@@ -164,7 +166,7 @@ def main():
     elapsed = time.perf_counter() - t0
     scan_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
     if world > 1:
-        t = torch.tensor([elapsed, scan_ms], dtype=torch.float64, device=dev if a.backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed, scan_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, scan_ms = float(t[0]), float(t[1])
     if a.check:  # the global top-k of the last step equals one whole-index search (exact)
@@ -202,6 +204,8 @@ def main():
                                f"GPU(s), {a.nq} queries/batch, brute-force top-{a.k}",
                    "rows": a.rows, "dim": a.dim, "nq": a.nq, "k": a.k, "parallelism": f"rowshard{world}",
                    "corpus_copies": copies,
+                   "exchange": ("RCCL all-gather from librfx (rfx_allgather_records)" if comm is not None else
+                                "host (gloo) rehearsal" if world > 1 else "none (one shard)"),
                    "scan_kernel": {0: "valu", 1: "mfma128", 2: "mfma256", 3: "mfma_qstationary128",
                                    4: "mfma_qstationary256", 5: "mfma_qstationary256_2wps"}[kern]},
         "achieved_hbm_gbps_per_gpu": round(achieved, 1),
@@ -221,7 +225,11 @@ def main():
         result["cpu_baseline"] = cpu_baseline(ix, q, a)
     if rank == 0:
         print(json.dumps(result), flush=True)
+    if comm is not None:
+        torch.cuda.synchronize()
+        comm.close()
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
     if not check_ok:
         raise SystemExit("oracle check of the last timed step FAILED (see oracle_check in the JSON line)")

@@ -94,6 +94,22 @@ int rfx_index_data(rfx_index_t h, void** out_ptr);
  * survive the process).  Format documented in DESIGN.md §Persistence. */
 int rfx_index_save(rfx_index_t h, const char* path);
 int rfx_index_load(const char* path, int device, rfx_index_t* out);
+/* Append-only row file of a store (§8b's rfx_index_open): the ingestion
+ * worker appends, the API processes load what was appended since their last look.  Format: a
+ * 64-byte header ("RFXROWS1", u32 version 1, u32 dim, u32 dtype, zero pad) then row-major rows
+ * of the dtype.  The file holds no row count: the writer publishes the committed count in the
+ * store manifest (rfx/store.py) once the rows are durable, and readers never read past it, so a
+ * torn tail is never read.  Tombstones travel separately (rfx/store.py tombs.bin).
+ * Index row i is file row file_base + i (a row-sharded store: each shard index holds a contiguous
+ * range of the file's rows; unsharded: file_base 0).
+ *   rfx_rows_append: write the index's rows [row0, rows) to file rows [file_base + row0, ...) (the
+ *     file is created, or cut to file_base + row0 rows first — a tail left by a crashed writer is
+ *     dropped), fsync.
+ *   rfx_rows_sync: append file rows [file_base + rows, file_base + upto) to the index (rows = the
+ *     index's current row count); a fresh index + rfx_rows_sync(h, path, n, base) opens a store or
+ *     one shard of it. */
+int rfx_rows_append(rfx_index_t h, const char* path, int64_t row0, int64_t file_base);
+int rfx_rows_sync(rfx_index_t h, const char* path, int64_t upto, int64_t file_base);
 
 /* ---- search ---------------------------------------------------------------------------------
  * Retrieval slice of ask_stream (gemini_rag.py:517-551; mock 673-694): brute-force inner
@@ -145,6 +161,24 @@ int rfx_topk_merge_records(const float* cand_scores_d, const void* cand_rows_d, 
                            void* out_records_d, void* stream);
 int rfx_merge_gathered(const void* records_d, int world, int64_t nq, int k, float* out_scores_d,
                        int64_t* out_rows_d, void* stream);
+
+/* ---- RCCL communicators (SURVEY §8b rfx_init "RCCL comm if n>1", §8e) --------------------------
+ * The all-gather of per-shard records runs on RCCL over xGMI from inside the library; the host
+ * language only bootstraps the communicator (passes the 128-byte id from rank 0 to the others).
+ *   one process per GPU: rank 0 rfx_comm_unique_id -> every rank rfx_comm_init_rank;
+ *   one process owning n GPUs (index server): rfx_comm_init_all (ncclCommInitAll).
+ * rfx_allgather_records: per local device i, sends_d[i] = [nq][k] records (rfx_topk_merge_records)
+ * and recvs_d[i] = [world][nq][k] records, ordered by rank, on streams[i] (arrays of n_local; a
+ * rank communicator has n_local = 1).  Then rfx_merge_gathered on the same stream. */
+#define RFX_COMM_ID_BYTES 128
+typedef uint64_t rfx_comm_t;
+int rfx_comm_unique_id(void* out_id /* RFX_COMM_ID_BYTES */);
+int rfx_comm_init_rank(int world, int rank, const void* unique_id, int device, rfx_comm_t* out);
+int rfx_comm_init_all(int n, const int* device_ids, rfx_comm_t* out);
+int rfx_comm_info(rfx_comm_t c, int* world, int* rank, int* n_local);
+int rfx_comm_destroy(rfx_comm_t c);
+int rfx_allgather_records(rfx_comm_t c, const void* const* sends_d, void* const* recvs_d, int64_t nq, int k,
+                          void* const* streams);
 
 /* ---- text → features (host) ---------------------------------------------------------------
  * The reference has no chunker/tokeniser of its own (chunking_config is forwarded to Gemini,

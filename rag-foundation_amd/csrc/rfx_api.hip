@@ -10,7 +10,14 @@
 // jobs per worker, worker.py:125).
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <cerrno>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -56,9 +63,26 @@ struct Index {
   int64_t live = 0;
   void* data = nullptr;
   std::vector<uint8_t> tomb;  // host bitmap (1 = deleted), mirrors the NaN rows on device
-  std::shared_mutex mu;
+  std::shared_timed_mutex mu;
   int64_t row_bytes() const { return (int64_t)dim * esize(dtype); }
 };
+
+// Bounded lock waits: a writer stuck behind long searches (or the reverse) gets RFX_EBUSY, which
+// the host maps to a TimeoutError so the reference's retry paths apply (gemini_rag.py:17-27,
+// ingestion.py:35-52).  RFX_LOCK_TIMEOUT_MS, default 30 s.
+std::chrono::milliseconds lock_timeout() {
+  static const long ms = [] {
+    const char* e = getenv("RFX_LOCK_TIMEOUT_MS");
+    return e && *e ? atol(e) : 30000L;
+  }();
+  return std::chrono::milliseconds(ms);
+}
+#define RFX_WLOCK(ix)                                                                            \
+  std::unique_lock<std::shared_timed_mutex> lk((ix)->mu, std::defer_lock);                        \
+  if (!lk.try_lock_for(lock_timeout())) return fail(RFX_EBUSY, "index busy: writer lock timed out")
+#define RFX_RLOCK(ix)                                                                            \
+  std::shared_lock<std::shared_timed_mutex> lk((ix)->mu, std::defer_lock);                        \
+  if (!lk.try_lock_for(lock_timeout())) return fail(RFX_EBUSY, "index busy: reader lock timed out")
 
 std::mutex g_reg_mu;
 std::map<uint64_t, std::shared_ptr<Index>> g_reg;
@@ -162,6 +186,58 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
 // query staging and thresholds live in the front of ws (q_off, tau_off < cs_off)
 size_t scan_ws_bytes(const SearchLayout& L) { return L.cs_off; }
 
+// ---- append-only row files (rfx/store.py) ----------------------------------------------------------
+constexpr int64_t kRowsHdr = 64;
+
+struct Fd {
+  int fd = -1;
+  ~Fd() {
+    if (fd >= 0) close(fd);
+  }
+};
+
+bool full_write(int fd, const uint8_t* p, size_t n) {
+  while (n) {
+    const ssize_t w = write(fd, p, n);
+    if (w < 0 && errno == EINTR) continue;
+    if (w <= 0) return false;
+    p += w;
+    n -= (size_t)w;
+  }
+  return true;
+}
+
+bool full_pread(int fd, uint8_t* p, size_t n, off_t off) {
+  while (n) {
+    const ssize_t r = pread(fd, p, n, off);
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) return false;
+    p += r;
+    off += r;
+    n -= (size_t)r;
+  }
+  return true;
+}
+
+void rows_header(const Index& ix, uint8_t hdr[kRowsHdr]) {
+  memset(hdr, 0, kRowsHdr);
+  memcpy(hdr, "RFXROWS1", 8);
+  const uint32_t v[3] = {1u, (uint32_t)ix.dim, (uint32_t)ix.dtype};
+  memcpy(hdr + 8, v, sizeof(v));
+}
+
+// pinned staging buffers for file <-> device copies
+struct Pinned {
+  void* p = nullptr;
+  explicit Pinned(size_t n) {
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) p = nullptr;
+  }
+  ~Pinned() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+constexpr size_t kStage = (size_t)64 << 20;
+
 // mask: optional row mask on the device (metadata filter), (rows + 31) / 32 words, checked by the
 // caller; every production scan kernel applies it in its epilogue.
 int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq, float* cs, int32_t* cr,
@@ -253,7 +329,7 @@ int rfx_index_destroy(rfx_index_t h) {
     ix = it->second;
     g_reg.erase(it);
   }
-  std::unique_lock<std::shared_mutex> lk(ix->mu);
+  std::unique_lock<std::shared_timed_mutex> lk(ix->mu);  // waits for in-flight searches: never EBUSY
   if (ix->data) {
     RFX_HIP(hipSetDevice(ix->device));
     RFX_HIP(hipFree(ix->data));
@@ -265,7 +341,7 @@ int rfx_index_destroy(rfx_index_t h) {
 int rfx_index_info(rfx_index_t h, int* dim, int* dtype, int64_t* rows, int64_t* capacity, int64_t* live_rows) {
   auto ix = get(h);
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
-  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  RFX_RLOCK(ix);
   if (dim) *dim = ix->dim;
   if (dtype) *dtype = ix->dtype;
   if (rows) *rows = ix->rows;
@@ -277,7 +353,7 @@ int rfx_index_info(rfx_index_t h, int* dim, int* dtype, int64_t* rows, int64_t* 
 int rfx_index_reserve(rfx_index_t h, int64_t capacity) {
   auto ix = get(h);
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
-  std::unique_lock<std::shared_mutex> lk(ix->mu);
+  RFX_WLOCK(ix);
   RFX_HIP(hipSetDevice(ix->device));
   return grow(*ix, capacity, nullptr);
 }
@@ -287,7 +363,7 @@ int rfx_index_add(rfx_index_t h, const void* vecs, int64_t n, int src_is_device,
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
   if (n < 0 || (n > 0 && !vecs)) return fail(RFX_EINVAL, "bad vectors");
   hipStream_t st = (hipStream_t)stream;
-  std::unique_lock<std::shared_mutex> lk(ix->mu);
+  RFX_WLOCK(ix);
   RFX_HIP(hipSetDevice(ix->device));
   int rc = grow(*ix, ix->rows + n, st);
   if (rc) return rc;
@@ -310,7 +386,7 @@ int rfx_index_add_synthetic(rfx_index_t h, uint64_t seed, int64_t gen_row0, int6
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
   if (n < 0) return fail(RFX_EINVAL, "n < 0");
   hipStream_t st = (hipStream_t)stream;
-  std::unique_lock<std::shared_mutex> lk(ix->mu);
+  RFX_WLOCK(ix);
   RFX_HIP(hipSetDevice(ix->device));
   int rc = grow(*ix, ix->rows + n, st);
   if (rc) return rc;
@@ -332,7 +408,7 @@ int rfx_index_tombstone(rfx_index_t h, const int64_t* rows_h, int64_t n, void* s
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
   if (n < 0 || (n > 0 && !rows_h)) return fail(RFX_EINVAL, "bad rows");
   hipStream_t st = (hipStream_t)stream;
-  std::unique_lock<std::shared_mutex> lk(ix->mu);
+  RFX_WLOCK(ix);
   std::vector<int64_t> todo;
   todo.reserve((size_t)n);
   for (int64_t i = 0; i < n; ++i) {
@@ -360,7 +436,7 @@ int rfx_index_tombstone(rfx_index_t h, const int64_t* rows_h, int64_t n, void* s
 int rfx_index_read(rfx_index_t h, int64_t row0, int64_t n, void* dst, int dst_is_device, void* stream) {
   auto ix = get(h);
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
-  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  RFX_RLOCK(ix);
   if (row0 < 0 || n < 0 || row0 + n > ix->rows) return fail(RFX_EINVAL, "rows [%lld, %lld) out of range", (long long)row0, (long long)(row0 + n));
   if (n == 0) return RFX_OK;
   if (!dst) return fail(RFX_EINVAL, "null destination");
@@ -384,7 +460,7 @@ int rfx_index_data(rfx_index_t h, void** out_ptr) {
 int rfx_index_save(rfx_index_t h, const char* path) {
   auto ix = get(h);
   if (!ix || !path) return fail(RFX_EINVAL, "unknown index handle / null path");
-  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  RFX_RLOCK(ix);
   RFX_HIP(hipSetDevice(ix->device));
   const std::string tmp = std::string(path) + ".tmp";
   FILE* f = fopen(tmp.c_str(), "wb");
@@ -462,11 +538,115 @@ int rfx_index_load(const char* path, int device, rfx_index_t* out) {
   return RFX_OK;
 }
 
+
+// ---- append-only row files (rfx/store.py) --------------------------------------------------------
+int rfx_rows_append(rfx_index_t h, const char* path, int64_t row0, int64_t file_base) {
+  auto ix = get(h);
+  if (!ix || !path) return fail(RFX_EINVAL, "unknown index handle / null path");
+  RFX_RLOCK(ix);
+  if (row0 < 0 || row0 > ix->rows) return fail(RFX_EINVAL, "row0 %lld outside [0, %lld]", (long long)row0, (long long)ix->rows);
+  if (file_base < 0) return fail(RFX_EINVAL, "file_base < 0");
+  RFX_HIP(hipSetDevice(ix->device));
+  Fd f;
+  f.fd = open(path, O_RDWR | O_CREAT | O_CLOEXEC, 0644);
+  if (f.fd < 0) return fail(RFX_EIO, "cannot open %s: %s", path, strerror(errno));
+  uint8_t hdr[kRowsHdr], want[kRowsHdr];
+  rows_header(*ix, want);
+  struct stat sb;
+  if (fstat(f.fd, &sb) != 0) return fail(RFX_EIO, "stat %s: %s", path, strerror(errno));
+  if (sb.st_size >= kRowsHdr) {
+    if (!full_pread(f.fd, hdr, kRowsHdr, 0) || memcmp(hdr, want, kRowsHdr) != 0)
+      return fail(RFX_EIO, "%s is not a row file of this index's dim/dtype", path);
+  } else if (file_base + row0 != 0) {
+    return fail(RFX_EIO, "%s holds no rows, cannot append at row %lld", path, (long long)(file_base + row0));
+  } else if (pwrite(f.fd, want, kRowsHdr, 0) != kRowsHdr) {
+    return fail(RFX_EIO, "header write to %s failed", path);
+  }
+  const int64_t rb = ix->row_bytes();
+  const off_t at = kRowsHdr + (file_base + row0) * rb;
+  if (sb.st_size < at) return fail(RFX_EIO, "%s holds fewer than %lld rows", path, (long long)(file_base + row0));
+  if (ftruncate(f.fd, at) != 0) return fail(RFX_EIO, "truncate %s: %s", path, strerror(errno));
+  if (lseek(f.fd, at, SEEK_SET) < 0) return fail(RFX_EIO, "seek %s failed", path);
+  const size_t total = (size_t)(ix->rows - row0) * rb;
+  if (total) {
+    Pinned buf(std::min(total, kStage));
+    if (!buf.p) return fail(RFX_ENOMEM, "pinned staging buffer");
+    for (size_t off = 0; off < total; off += kStage) {
+      const size_t nb = std::min(kStage, total - off);
+      RFX_HIP(hipMemcpy(buf.p, (uint8_t*)ix->data + row0 * rb + off, nb, hipMemcpyDeviceToHost));
+      if (!full_write(f.fd, (const uint8_t*)buf.p, nb)) return fail(RFX_EIO, "write to %s failed", path);
+    }
+  }
+  if (fsync(f.fd) != 0) return fail(RFX_EIO, "fsync %s: %s", path, strerror(errno));
+  return RFX_OK;
+}
+
+int rfx_rows_sync(rfx_index_t h, const char* path, int64_t upto, int64_t file_base) {
+  auto ix = get(h);
+  if (!ix || !path) return fail(RFX_EINVAL, "unknown index handle / null path");
+  RFX_WLOCK(ix);
+  if (upto < ix->rows) return fail(RFX_EINVAL, "upto %lld < rows %lld", (long long)upto, (long long)ix->rows);
+  if (upto == ix->rows) return RFX_OK;
+  if (file_base < 0) return fail(RFX_EINVAL, "file_base < 0");
+  RFX_HIP(hipSetDevice(ix->device));
+  Fd f;
+  f.fd = open(path, O_RDONLY | O_CLOEXEC);
+  if (f.fd < 0) return fail(RFX_EIO, "cannot open %s: %s", path, strerror(errno));
+  uint8_t hdr[kRowsHdr], want[kRowsHdr];
+  rows_header(*ix, want);
+  if (!full_pread(f.fd, hdr, kRowsHdr, 0) || memcmp(hdr, want, kRowsHdr) != 0)
+    return fail(RFX_EIO, "%s is not a row file of this index's dim/dtype", path);
+  const int64_t rb = ix->row_bytes();
+  struct stat sb;
+  if (fstat(f.fd, &sb) != 0 || sb.st_size < kRowsHdr + (file_base + upto) * rb)
+    return fail(RFX_EIO, "%s holds fewer than %lld rows", path, (long long)(file_base + upto));
+  int rc = grow(*ix, upto, nullptr);
+  if (rc) return rc;
+  // two pinned buffers: read the next block from the file while the previous one is copied up
+  const size_t total = (size_t)(upto - ix->rows) * rb;
+  Pinned b0(std::min(total, kStage)), b1(std::min(total, kStage));
+  if (!b0.p || !b1.p) return fail(RFX_ENOMEM, "pinned staging buffers");
+  hipStream_t st;
+  RFX_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  hipEvent_t ev[2];
+  RFX_HIP(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+  RFX_HIP(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+  void* bufs[2] = {b0.p, b1.p};
+  bool used[2] = {false, false};
+  const off_t src0 = kRowsHdr + (file_base + ix->rows) * rb;
+  uint8_t* dst0 = (uint8_t*)ix->data + ix->rows * rb;
+  int err = RFX_OK;
+  for (size_t off = 0, i = 0; off < total && err == RFX_OK; off += kStage, i ^= 1) {
+    const size_t nb = std::min(kStage, total - off);
+    if (used[i] && hipEventSynchronize(ev[i]) != hipSuccess) err = fail(RFX_EDEVICE, "staging event");
+    if (err == RFX_OK && !full_pread(f.fd, (uint8_t*)bufs[i], nb, src0 + (off_t)off))
+      err = fail(RFX_EIO, "read from %s failed", path);
+    if (err == RFX_OK && (hipMemcpyAsync(dst0 + off, bufs[i], nb, hipMemcpyHostToDevice, st) != hipSuccess ||
+                          hipEventRecord(ev[i], st) != hipSuccess))
+      err = fail(RFX_EDEVICE, "H2D copy failed");
+    used[i] = true;
+  }
+  if (hipStreamSynchronize(st) != hipSuccess && err == RFX_OK) err = fail(RFX_EDEVICE, "H2D copy failed");
+  (void)hipEventDestroy(ev[0]);
+  (void)hipEventDestroy(ev[1]);
+  (void)hipStreamDestroy(st);
+  if (err) {
+    // rows beyond ix->rows may be partly written: restore the NaN tail invariant
+    fill_tail_nan(*ix, nullptr);
+    return err;
+  }
+  const int64_t n = upto - ix->rows;
+  ix->rows = upto;
+  ix->live += n;
+  ix->tomb.resize((size_t)(ix->rows + 7) / 8, 0);
+  return RFX_OK;
+}
+
 // ---- search ---------------------------------------------------------------------------------------
 int rfx_search_workspace_bytes(rfx_index_t h, int64_t nq, int k, size_t* out_bytes) {
   auto ix = get(h);
   if (!ix || !out_bytes) return fail(RFX_EINVAL, "unknown index handle / null out");
-  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  RFX_RLOCK(ix);
   SearchLayout L;
   int rc = make_layout(*ix, nq, k, L);
   if (rc) return rc;
@@ -477,7 +657,7 @@ int rfx_search_workspace_bytes(rfx_index_t h, int64_t nq, int k, size_t* out_byt
 int rfx_scan_plan(rfx_index_t h, int64_t nq, int k, int* out_kernel, int64_t* out_n_cand) {
   auto ix = get(h);
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
-  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  RFX_RLOCK(ix);
   SearchLayout L;
   int rc = make_layout(*ix, nq, k, L);
   if (rc) return rc;
@@ -496,7 +676,7 @@ int rfx_scan_topk_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k
                          void* stream) {
   auto ix = get(h);
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
-  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  RFX_RLOCK(ix);
   SearchLayout L;
   int rc = make_layout(*ix, nq, k, L);
   if (rc) return rc;
@@ -525,7 +705,7 @@ int rfx_scan_list_len(rfx_index_t h, int64_t nq, int k, int* out_list_len) {
   auto ix = get(h);
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
   if (!out_list_len) return fail(RFX_EINVAL, "null out");
-  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  RFX_RLOCK(ix);
   SearchLayout L;
   int rc = make_layout(*ix, nq, k, L);
   if (rc) return rc;
@@ -580,7 +760,7 @@ int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k
                          void* ws_d, size_t ws_bytes, void* stream) {
   auto ix = get(h);
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
-  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  RFX_RLOCK(ix);
   SearchLayout L;
   int rc = make_layout(*ix, nq, k, L);
   if (rc) return rc;
@@ -613,7 +793,7 @@ int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k
 int rfx_dbg_stream_read(rfx_index_t h, void* scratch4_d, void* stream) {
   auto ix = get(h);
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
-  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  RFX_RLOCK(ix);
   rfx::launch_stream_read(ix->data, ix->rows * ix->row_bytes(), (uint32_t*)scratch4_d, (hipStream_t)stream);
   RFX_HIP(hipGetLastError());
   return RFX_OK;
@@ -631,7 +811,7 @@ int rfx_search_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k, c
                       void* stream) {
   auto ix = get(h);
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
-  std::shared_lock<std::shared_mutex> lk(ix->mu);
+  RFX_RLOCK(ix);
   SearchLayout L;
   int rc = make_layout(*ix, nq, k, L);
   if (rc) return rc;

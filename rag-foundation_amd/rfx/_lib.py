@@ -104,6 +104,14 @@ SIGNATURES = {
     "rfx_index_data": ([_u64, _pp], _i),
     "rfx_index_save": ([_u64, _cs], _i),
     "rfx_index_load": ([_cs, _i, _pu64], _i),
+    "rfx_rows_append": ([_u64, _cs, _i64, _i64], _i),
+    "rfx_rows_sync": ([_u64, _cs, _i64, _i64], _i),
+    "rfx_comm_unique_id": ([_p], _i),
+    "rfx_comm_init_rank": ([_i, _i, _p, _i, _pu64], _i),
+    "rfx_comm_init_all": ([_i, _p, _pu64], _i),
+    "rfx_comm_info": ([_u64, _pi, _pi, _pi], _i),
+    "rfx_comm_destroy": ([_u64], _i),
+    "rfx_allgather_records": ([_u64, _p, _p, _i64, _i, _p], _i),
     "rfx_search_workspace_bytes": ([_u64, _i64, _i, _psz], _i),
     "rfx_search": ([_u64, _p, _i64, _i, _p, _p, _p, _sz, _p], _i),
     "rfx_scan_plan": ([_u64, _i64, _i, _pi, _pi64], _i),

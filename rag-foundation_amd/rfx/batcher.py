@@ -11,8 +11,15 @@ and when it finishes leadership passes to the oldest of them, which runs the nex
 timer, no background thread (safe across gunicorn forks): an idle process adds no latency, a busy
 one forms batches as large as the queue that built up during the previous launch.
 """
+import os
 import threading
 from typing import Any, Callable, List, Sequence
+
+
+class BatchTimeout(TimeoutError):
+    """A waiter gave up: the batch ahead of it did not finish in time.  A TimeoutError, so the
+    reference's retry paths apply (RETRYABLE_EXCEPTIONS, gemini_rag.py:17-27; chat retries before
+    the first delta, chat.py:1076-1128)."""
 
 
 class _Slot:
@@ -26,12 +33,15 @@ class _Slot:
 
 
 class GroupBatcher:
-    def __init__(self, run: Callable[[Sequence[Any]], List[Any]], max_batch: int = 256):
-        """run(items) -> results, one per item, in order; called by one thread at a time."""
+    def __init__(self, run: Callable[[Sequence[Any]], List[Any]], max_batch: int = 256, timeout: float = None):
+        """run(items) -> results, one per item, in order; called by one thread at a time.
+        timeout: longest a request waits for the batches ahead of it (RFX_BATCH_TIMEOUT_S, 30 s)
+        before it raises BatchTimeout; a request that is running its own batch is not cut off."""
         if max_batch < 1:
             raise ValueError("max_batch must be >= 1")
         self._run = run
         self.max_batch = int(max_batch)
+        self.timeout = float(os.environ.get("RFX_BATCH_TIMEOUT_S", "30")) if timeout is None else float(timeout)
         self._lock = threading.Lock()
         self._queue: List[tuple] = []
         self._busy = False
@@ -45,7 +55,15 @@ class GroupBatcher:
             lead = not self._busy
             self._busy = True
         if not lead:
-            slot.event.wait()
+            if not slot.event.wait(self.timeout):
+                with self._lock:
+                    queued = any(s is slot for _, s in self._queue)
+                    if queued and not slot.lead:
+                        self._queue = [(it, s) for it, s in self._queue if s is not slot]
+                        raise BatchTimeout(f"search queue: no batch slot within {self.timeout:.0f} s")
+                # handed the lead at the deadline, or already inside a running batch
+                if not slot.lead and not slot.event.wait(self.timeout):
+                    raise BatchTimeout(f"search batch did not finish within {2 * self.timeout:.0f} s")
             if not slot.lead:
                 return self._value(slot)
             slot.event.clear()

@@ -40,6 +40,21 @@ class DeviceIndex:
     def save(self, path: str) -> None:
         check(lib.rfx_index_save(self.handle, path.encode()))
 
+    def rows_append(self, path: str, row0: int, file_base: int = 0) -> None:
+        """Write rows [row0, rows) to the store's append-only row file (fsync'ed); index row i is
+        file row file_base + i."""
+        with torch.cuda.device(self.device):
+            check(lib.rfx_rows_append(self.handle, path.encode(), int(row0), int(file_base)))
+
+    def rows_sync(self, path: str, upto: int, file_base: int = 0) -> None:
+        """Append file rows [file_base + rows, file_base + upto) written by another process."""
+        with torch.cuda.device(self.device):
+            check(lib.rfx_rows_sync(self.handle, path.encode(), int(upto), int(file_base)))
+
+    def mask_tensor(self, words):
+        """Row-mask words (numpy int32) as the device tensor the masked search takes."""
+        return torch.from_numpy(words).to(self._dev())
+
     def close(self) -> None:
         if getattr(self, "handle", None):
             check(lib.rfx_index_destroy(self.handle))

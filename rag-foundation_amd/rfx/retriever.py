@@ -40,7 +40,13 @@ def _chunking(cfg):
 # (device, dim) and per store — or no two requests would ever share a batch.
 _STATE_LOCK = threading.Lock()
 _EMBEDDERS = {}
-_BATCHERS = {}
+_BATCHERS = {}  # (store name, filter key, registry id) -> GroupBatcher
+
+
+def _purge_batchers(name):
+    with _STATE_LOCK:
+        for key in [k for k in _BATCHERS if k[0] == name]:
+            del _BATCHERS[key]
 
 
 class GpuRetriever:
@@ -69,9 +75,7 @@ class GpuRetriever:
         return self.registry.create(display_name, self.dim, self.dtype).name
 
     def drop_store(self, name):
-        with _STATE_LOCK:
-            for key in [k for k in _BATCHERS if k[0] == name]:
-                del _BATCHERS[key]
+        _purge_batchers(name)
         return self.registry.drop(name)
 
     def store_names(self):
@@ -103,30 +107,39 @@ class GpuRetriever:
             s, r = s.cpu().tolist(), r.cpu().tolist()
         return [(s[i][:k], r[i][:k]) for i, (_, k) in enumerate(items)]
 
-    def _batcher(self, st, fkey, row_mask):
+    def _run_batch(self, name, metadata_filter, items):
+        """Batch runner: resolves the store and its row mask when the batch runs (a batcher holds
+        no LocalStore, so a store that another process replaced or dropped is freed here too)."""
+        st = self.registry.get(name)
+        if st is None:
+            return [None] * len(items)
+        mask = st.row_mask(metadata_filter) if metadata_filter is not None else None
+        if metadata_filter is not None and mask is None:
+            return [None] * len(items)
+        return [(st, s, r) for s, r in self._search_store_batch(st, items, mask)]
+
+    def _batcher(self, name, metadata_filter):
         # one batcher per (store, filter): a launch applies one row mask to all its queries
-        key = (st.name, id(st), fkey, st.version)
+        key = (name, filters.filter_key(metadata_filter), id(self.registry))
         with _STATE_LOCK:
             b = _BATCHERS.get(key)
             if b is None:
-                b = GroupBatcher(lambda items, st=st, m=row_mask: self._search_store_batch(st, items, m),
+                if self.registry.on_evict.count(_purge_batchers) == 0:
+                    self.registry.on_evict.append(_purge_batchers)
+                b = GroupBatcher(lambda items, n=name, f=metadata_filter: self._run_batch(n, f, items),
                                  max_batch=256)
-                for old in [k for k in _BATCHERS if k[:3] == key[:3]]:
-                    del _BATCHERS[old]  # an older version's mask
-                if len(_BATCHERS) >= 1024:
+                if len(_BATCHERS) >= 4096:
                     _BATCHERS.clear()
                 _BATCHERS[key] = b
             return b
 
-    def search_store(self, st, question, k, metadata_filter=None):
-        """(scores, rows) of one question against one store, or None when the filter selects no
-        row of it; batched with concurrent callers of the same store and filter."""
-        mask = st.row_mask(metadata_filter) if metadata_filter is not None else None
-        if metadata_filter is not None and mask is None:
-            return None
+    def search_store(self, name, question, k, metadata_filter=None):
+        """(store, scores, rows) of one question against one store, or None when the store is
+        gone or the filter selects no row of it; batched with concurrent callers of the same
+        store and filter."""
         if self.batching:
-            return self._batcher(st, filters.filter_key(metadata_filter), mask).submit((question, int(k)))
-        return self._search_store_batch(st, [(question, int(k))], mask)[0]
+            return self._batcher(name, metadata_filter).submit((question, int(k)))
+        return self._run_batch(name, metadata_filter, [(question, int(k))])[0]
 
     def search(self, store_names, question, k, metadata_filter=None):
         """Top-k hits over the union of the named stores, rank order (score desc, store order,
@@ -140,14 +153,15 @@ class GpuRetriever:
             st = self.registry.get(name)
             if st is None or st.index.rows == 0:
                 continue
-            res = self.search_store(st, question, k, filt)
+            res = self.search_store(name, question, k, filt)
             if res is None:
                 continue
-            s, r = res
+            st, s, r = res
             for sc, row in zip(s, r):
-                if row < 0:
+                info = st.row_info(row) if row >= 0 else None
+                if info is None:
                     continue
-                fid, text, title, uri = st.row_info(row)
+                fid, text, title, uri = info
                 hits.append((-sc, si, row, Hit(sc, name, row, fid, text, title, uri)))
         hits.sort(key=lambda h: h[:3])
         return [h[3] for h in hits[:k]]

@@ -1,123 +1,313 @@
 """Local File-Search-store equivalent: a DeviceIndex plus per-row chunk metadata, persisted on
-disk so that the API processes can serve what the ingestion worker wrote (the worker deletes the
-uploaded file after indexing, backend/app/services/ingestion.py:341).
+disk so that the API processes serve what the ingestion worker wrote (the worker deletes the
+uploaded file after indexing, backend/app/services/ingestion.py:341) — SURVEY §8f item 1.
 
-On-disk layout of a store (directory <root>/<store id>/):
-  manifest.json   {"name", "display_name", "dim", "dtype", "version", "files": {file_id: {...}}}
-  index.rfx       rfx_index_save() image (rows + tombstones)
-  meta.jsonl      one JSON object per row: {"f": file_id, "t": chunk text}
+On-disk layout of a store (directory <root>/<store id>/), every data file APPEND-ONLY:
+  rows.rfx      rfx_rows_append() row file: 64-byte header + row-major rows (C ABI, include/rfx.h)
+  meta.jsonl    one JSON object per row: {"f": file_id, "t": chunk text}
+  files.jsonl   file records: {"op": "add", "id", "first", "n", "display_name", "uri", "metadata"}
+                and {"op": "del", "id"}
+  tombs.bin     int64 row ids of deleted rows
+  manifest.json the commit point: {"format": 2, "name", "display_name", "dim", "dtype",
+                "generation", "version", "rows", "meta_bytes", "files_bytes", "tombs"} — the
+                committed length of every file above; replaced atomically (rename) after the
+                appended bytes are fsync'ed.  Readers never read past it, so a writer that dies
+                mid-append leaves a tail that is ignored, and cut by the next writer.
+  .lock         fcntl writer lock: appends from several processes (ARQ worker max_jobs=10,
+                worker.py:125; several workers) serialise on it, each first catching up with
+                what the others committed.
+An upload costs O(its own rows) of disk and device work; a reader (API process) that sees a
+newer manifest loads only what was appended since its last look (rows, metadata, tombstones).
+
 GPU state is a process-level singleton (StoreRegistry), because get_rag_client() builds a new
 adapter per request (chat.py:937, ingestion.py:214).
 """
+import errno
+import fcntl
 import json
 import os
 import shutil
 import threading
+import time
 import uuid
 
-import torch
+import numpy as np
 
 from . import filters
+from ._lib import RFX_EBUSY, RfxTransientError
 from .index import DeviceIndex
 
 STORE_PREFIX = "fileSearchStores/"  # accepted by routes/stores.py:46 (prefix check)
+FORMAT = 2
 
 
 def default_root() -> str:
     return os.environ.get("RFX_INDEX_DIR", os.path.join(os.path.expanduser("~"), ".cache", "rfx", "stores"))
 
 
+def _fsync_dir(path):
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
+
+def _append(path, committed, data: bytes) -> int:
+    """Cut `path` to its committed length (drops a crashed writer's tail), append data, fsync.
+    Returns the new committed length."""
+    fd = os.open(path, os.O_RDWR | os.O_CREAT | os.O_CLOEXEC, 0o644)
+    try:
+        os.ftruncate(fd, committed)
+        os.lseek(fd, committed, os.SEEK_SET)
+        view = memoryview(data)
+        while view:
+            n = os.write(fd, view)
+            view = view[n:]
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+    return committed + len(data)
+
+
+def _read_range(path, start, end) -> bytes:
+    if end <= start:
+        return b""
+    with open(path, "rb") as f:
+        f.seek(start)
+        b = f.read(end - start)
+    if len(b) != end - start:
+        raise OSError(errno.EIO, f"{path}: committed range [{start}, {end}) is missing")
+    return b
+
+
+class StoreGone(Exception):
+    """The store's manifest no longer exists (dropped by another process)."""
+
+
 class LocalStore:
-    def __init__(self, name, display_name, dim, dtype, device, path):
-        self.name, self.display_name = name, display_name
-        self.dim, self.dtype, self.device, self.path = dim, dtype, device, path
-        self.index = DeviceIndex(dim, dtype, device)
+    # the vector store behind a LocalStore: DeviceIndex (HIP) in the product; tests inject a host
+    # stand-in with the same interface to exercise the file protocol without a GPU
+    index_factory = DeviceIndex
+
+    def __init__(self, path, device, index_factory=None):
+        self.path, self.device = path, int(device)
+        if index_factory is not None:
+            self.index_factory = index_factory
+        self.name = self.display_name = None
+        self.dim = self.dtype = None
+        self.generation = None
+        self.index = None
         self.rows = []      # per row: (file_id, chunk text)
         self.files = {}     # file_id -> {"first", "n", "display_name", "uri", "deleted", "metadata"}
-        self.version = 0
+        self.version = -1
+        self.meta_bytes = self.files_bytes = self.tombs = 0
         self.lock = threading.RLock()
-        self._mtime = None
+        self._stat = None
         self._masks = {}    # (version, filter key) -> device row mask
 
-    # ---- persistence ------------------------------------------------------------------------
-    def _manifest(self):
-        return {"name": self.name, "display_name": self.display_name, "dim": self.dim, "dtype": self.dtype,
-                "version": self.version, "rows": len(self.rows), "files": self.files}
+    # ---- files -------------------------------------------------------------------------------
+    def _p(self, name):
+        return os.path.join(self.path, name)
 
-    def save(self):
-        os.makedirs(self.path, exist_ok=True)
-        self.index.save(os.path.join(self.path, "index.rfx"))
-        tmp = os.path.join(self.path, "meta.jsonl.tmp")
-        with open(tmp, "w", encoding="utf-8") as f:
-            for fid, text in self.rows:
-                f.write(json.dumps({"f": fid, "t": text}, ensure_ascii=False) + "\n")
-        os.replace(tmp, os.path.join(self.path, "meta.jsonl"))
-        tmp = os.path.join(self.path, "manifest.json.tmp")
-        with open(tmp, "w", encoding="utf-8") as f:
-            json.dump(self._manifest(), f)
-        os.replace(tmp, os.path.join(self.path, "manifest.json"))
-        self._mtime = os.stat(os.path.join(self.path, "manifest.json")).st_mtime_ns
+    def _read_manifest(self):
+        try:
+            with open(self._p("manifest.json"), encoding="utf-8") as f:
+                st = os.fstat(f.fileno())
+                man = json.load(f)
+        except FileNotFoundError:
+            return None, None
+        if man.get("format") != FORMAT:
+            raise RuntimeError(f"{self.path}: store format {man.get('format')} != {FORMAT}")
+        return man, (st.st_ino, st.st_mtime_ns, st.st_size)
 
+    def _write_manifest(self):
+        man = {"format": FORMAT, "name": self.name, "display_name": self.display_name, "dim": self.dim,
+               "dtype": self.dtype, "generation": self.generation, "version": self.version,
+               "rows": len(self.rows), "meta_bytes": self.meta_bytes, "files_bytes": self.files_bytes,
+               "tombs": self.tombs}
+        tmp = self._p(f"manifest.json.{os.getpid()}.{threading.get_ident()}.tmp")
+        with open(tmp, "w", encoding="utf-8") as f:
+            json.dump(man, f)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, self._p("manifest.json"))
+        _fsync_dir(self.path)
+        st = os.stat(self._p("manifest.json"))
+        self._stat = (st.st_ino, st.st_mtime_ns, st.st_size)
+
+    class _WriterLock:
+        """fcntl lock on <store>/.lock, bounded wait -> RfxTransientError (a TimeoutError: the
+        ingestion retry, ingestion.py:35-52, and RETRYABLE_EXCEPTIONS, gemini_rag.py:17-27)."""
+
+        def __init__(self, store):
+            self.path = store._p(".lock")
+            self.timeout = float(os.environ.get("RFX_LOCK_TIMEOUT_S", "30"))
+
+        def __enter__(self):
+            try:
+                self.fd = os.open(self.path, os.O_RDWR | os.O_CREAT | os.O_CLOEXEC, 0o644)
+            except FileNotFoundError:
+                raise StoreGone(self.path)
+            t_end = time.monotonic() + self.timeout
+            while True:
+                try:
+                    fcntl.flock(self.fd, fcntl.LOCK_EX | fcntl.LOCK_NB)
+                    return self
+                except BlockingIOError:
+                    if time.monotonic() >= t_end:
+                        os.close(self.fd)
+                        raise RfxTransientError(RFX_EBUSY, f"store writer lock {self.path} busy "
+                                                           f"for {self.timeout:.0f} s")
+                    time.sleep(0.005)
+
+        def __exit__(self, *exc):
+            fcntl.flock(self.fd, fcntl.LOCK_UN)
+            os.close(self.fd)
+
+    # ---- create / open / catch up ---------------------------------------------------------------
     @classmethod
-    def load(cls, path, device):
-        with open(os.path.join(path, "manifest.json"), encoding="utf-8") as f:
-            man = json.load(f)
-        st = cls.__new__(cls)
-        st.name, st.display_name = man["name"], man["display_name"]
-        st.dim, st.dtype, st.device, st.path = man["dim"], man["dtype"], device, path
-        st.version = man["version"]
-        st.files = man["files"]
-        st.lock = threading.RLock()
-        st._masks = {}
-        idx = os.path.join(path, "index.rfx")
-        st.index = DeviceIndex.load(idx, device) if os.path.exists(idx) else DeviceIndex(st.dim, st.dtype, device)
-        st.rows = []
-        meta = os.path.join(path, "meta.jsonl")
-        if os.path.exists(meta):
-            with open(meta, encoding="utf-8") as f:
-                for line in f:
-                    o = json.loads(line)
-                    st.rows.append((o["f"], o["t"]))
-        st._mtime = os.stat(os.path.join(path, "manifest.json")).st_mtime_ns
+    def create(cls, path, name, display_name, dim, dtype, device, index_factory=None):
+        os.makedirs(path, exist_ok=False)
+        st = cls(path, device, index_factory)
+        st.name, st.display_name, st.dim, st.dtype = name, display_name, int(dim), dtype
+        st.generation = uuid.uuid4().hex
+        st.index = st.index_factory(st.dim, dtype, st.device)
+        st.version = 0
+        with st._WriterLock(st):
+            st._write_manifest()
         return st
 
-    def stale(self) -> bool:
-        try:
-            return os.stat(os.path.join(self.path, "manifest.json")).st_mtime_ns != self._mtime
-        except FileNotFoundError:
-            return False
+    @classmethod
+    def open(cls, path, device, index_factory=None):
+        st = cls(path, device, index_factory)
+        with st.lock:
+            st._sync()
+        return st
 
-    # ---- writes ------------------------------------------------------------------------------
-    def add_document(self, chunks, vecs, display_name, metadata=None):
+    def _reset(self, man):
+        self.name, self.display_name = man["name"], man["display_name"]
+        self.dim, self.dtype = int(man["dim"]), man["dtype"]
+        self.generation = man["generation"]
+        if self.index is not None:
+            self.index.close()
+        self.index = self.index_factory(self.dim, self.dtype, self.device)
+        self.rows, self.files = [], {}
+        self.meta_bytes = self.files_bytes = self.tombs = 0
+        self.version = -1
+        self._masks = {}
+
+    def _sync(self, man=None, stat=None):
+        """Catch up with the committed state on disk (caller holds self.lock).  Incremental: only
+        what was appended since the last sync is read."""
+        if man is None:
+            man, stat = self._read_manifest()
+        if man is None:
+            raise StoreGone(self.path)
+        if man["generation"] != self.generation:
+            self._reset(man)
+        if man["version"] == self.version:
+            self._stat = stat
+            return
+        n_rows = int(man["rows"])
+        if n_rows < len(self.rows) or man["meta_bytes"] < self.meta_bytes or man["files_bytes"] < self.files_bytes \
+                or man["tombs"] < self.tombs:
+            raise RuntimeError(f"{self.path}: committed state went backwards (same generation)")
+        if n_rows > self.index.rows:
+            self.index.rows_sync(self._p("rows.rfx"), n_rows)
+        for line in _read_range(self._p("meta.jsonl"), self.meta_bytes, man["meta_bytes"]).splitlines():
+            o = json.loads(line)
+            self.rows.append((o["f"], o["t"]))
+        for line in _read_range(self._p("files.jsonl"), self.files_bytes, man["files_bytes"]).splitlines():
+            self._apply_file_record(json.loads(line))
+        if man["tombs"] > self.tombs:
+            raw = _read_range(self._p("tombs.bin"), 8 * self.tombs, 8 * man["tombs"])
+            self.index.tombstone(np.frombuffer(raw, dtype="<i8"))
+        if len(self.rows) != n_rows or self.index.rows != n_rows:
+            raise RuntimeError(f"{self.path}: {len(self.rows)} metadata rows / {self.index.rows} vectors, "
+                               f"manifest says {n_rows}")
+        self.meta_bytes, self.files_bytes, self.tombs = man["meta_bytes"], man["files_bytes"], man["tombs"]
+        self.version = man["version"]
+        self._stat = stat
+
+    def _apply_file_record(self, r):
+        if r["op"] == "add":
+            self.files[r["id"]] = {"first": r["first"], "n": r["n"], "display_name": r["display_name"],
+                                   "uri": r["uri"], "deleted": False, "metadata": r.get("metadata")}
+        elif r["op"] == "del" and r["id"] in self.files:
+            self.files[r["id"]]["deleted"] = True
+
+    def stale(self) -> bool:
+        """True when the manifest changed (or vanished) since this process last synced."""
+        try:
+            st = os.stat(self._p("manifest.json"))
+        except FileNotFoundError:
+            return True
+        return (st.st_ino, st.st_mtime_ns, st.st_size) != self._stat
+
+    def refresh(self) -> bool:
+        """Catch up if another process committed; False when the store is gone."""
         with self.lock:
+            try:
+                self._sync()
+            except StoreGone:
+                return False
+            return True
+
+    # ---- writes (exclusive across processes) ------------------------------------------------------
+    def add_document(self, chunks, vecs, display_name, metadata=None):
+        with self.lock, self._WriterLock(self):
+            self._sync()  # append at the end of what every writer committed
             file_id = f"files/local-{uuid.uuid4().hex}"
-            first = self.index.add(vecs) if len(chunks) else self.index.rows
-            for c in chunks:
-                self.rows.append((file_id, c))
-            self.files[file_id] = {"first": first, "n": len(chunks), "display_name": display_name,
-                                   "uri": f"local://{self.name}/{file_id}", "deleted": False,
-                                   "metadata": metadata or None}
+            first = self.index.rows
+            if len(chunks):
+                self.index.add(vecs)
+                try:
+                    self.index.rows_append(self._p("rows.rfx"), first)
+                    meta = "".join(json.dumps({"f": file_id, "t": c}, ensure_ascii=False) + "\n" for c in chunks)
+                    self.meta_bytes = _append(self._p("meta.jsonl"), self.meta_bytes, meta.encode())
+                except BaseException:
+                    self._rollback(first)
+                    raise
+            rec = {"op": "add", "id": file_id, "first": first, "n": len(chunks), "display_name": display_name,
+                   "uri": f"local://{self.name}/{file_id}", "metadata": metadata or None}
+            self.files_bytes = _append(self._p("files.jsonl"), self.files_bytes, (json.dumps(rec) + "\n").encode())
+            self._apply_file_record(rec)
+            self.rows.extend((file_id, c) for c in chunks)
             self.version += 1
-            self.save()
+            self._write_manifest()
             return file_id, first
 
+    def _rollback(self, first):
+        """A failed append: drop this process's uncommitted device rows by re-opening from disk."""
+        man, stat = self._read_manifest()
+        self.generation = None
+        self._sync(man, stat)
+
     def delete_file(self, file_id) -> bool:
-        with self.lock:
+        with self.lock, self._WriterLock(self):
+            self._sync()
             f = self.files.get(file_id)
             if not f or f["deleted"]:
                 return False
             if f["n"]:
-                self.index.tombstone(range(f["first"], f["first"] + f["n"]))
-            f["deleted"] = True
+                rows = np.arange(f["first"], f["first"] + f["n"], dtype="<i8")
+                self.index.tombstone(rows)
+                _append(self._p("tombs.bin"), 8 * self.tombs, rows.tobytes())
+                self.tombs += len(rows)
+            rec = {"op": "del", "id": file_id}
+            self.files_bytes = _append(self._p("files.jsonl"), self.files_bytes, (json.dumps(rec) + "\n").encode())
+            self._apply_file_record(rec)
             self.version += 1
-            self.save()
+            self._write_manifest()
             return True
 
+    # ---- reads -------------------------------------------------------------------------------------
     def row_mask(self, metadata_filter):
         """Device row mask (int32 words) of the live files whose upload metadata matches the
         filter (rfx.filters), or None when no file matches.  Cached per (store version, filter)."""
-        key = (self.version, filters.filter_key(metadata_filter))
         with self.lock:
+            key = (self.version, filters.filter_key(metadata_filter))
             if key in self._masks:
                 return self._masks[key]
             ranges = [(f["first"], f["n"]) for f in self.files.values()
@@ -126,26 +316,47 @@ class LocalStore:
             mask = None
             if ranges:
                 words = filters.row_mask_words(self.index.rows, ranges)
-                mask = torch.from_numpy(words).to(f"cuda:{self.device}")
+                mask = self.index.mask_tensor(words)
             if len(self._masks) >= 64:
                 self._masks.clear()
             self._masks[key] = mask
             return mask
 
     def row_info(self, row):
+        """(file_id, chunk text, title, uri) of a row, or None for a row this process has no
+        metadata for (cannot happen after a consistent sync; guarded anyway)."""
+        if not 0 <= row < len(self.rows):
+            return None
         fid, text = self.rows[row]
         f = self.files.get(fid, {})
         return fid, text, f.get("display_name"), f.get("uri")
 
+    def close(self):
+        with self.lock:
+            if self.index is not None:
+                self.index.close()
+
 
 class StoreRegistry:
-    """Process-wide map store name -> LocalStore (lazy load, reload when another process wrote)."""
+    """Process-wide map store name -> LocalStore: lazy open, incremental catch-up when another
+    process committed, eviction when another process dropped the store."""
 
-    def __init__(self, root=None, device=None):
+    def __init__(self, root=None, device=None, index_factory=None, devices=None):
+        """devices (or RFX_DEVICES, e.g. "0,1,2,3,4,5,6,7"; "0x4" = 4 logical shards on device 0):
+        more than one -> every store is row-sharded over them (rfx.sharded.ShardedIndex)."""
         self.root = root or default_root()
+        self.index_factory = index_factory
         self.device = int(os.environ.get("RFX_DEVICE", "0")) if device is None else int(device)
+        spec = devices if devices is not None else os.environ.get("RFX_DEVICES")
+        if index_factory is None and spec:
+            from .sharded import ShardedIndex, parse_devices
+            devs = parse_devices(spec) if isinstance(spec, str) else [int(d) for d in spec]
+            if len(devs) > 1:
+                self.device = devs[0]
+                self.index_factory = lambda dim, dtype, device, _d=tuple(devs): ShardedIndex(dim, dtype, list(_d))
         self._stores = {}
         self._lock = threading.Lock()
+        self.on_evict = []  # callbacks(name) when a store leaves this registry (rfx.retriever)
 
     def _dir(self, name):
         if not isinstance(name, str) or not name.startswith(STORE_PREFIX + "local-"):
@@ -154,34 +365,53 @@ class StoreRegistry:
 
     def create(self, display_name, dim, dtype):
         name = f"{STORE_PREFIX}local-{uuid.uuid4().hex}"
-        st = LocalStore(name, display_name, dim, dtype, self.device, self._dir(name))
-        st.save()
+        os.makedirs(self.root, exist_ok=True)
+        st = LocalStore.create(self._dir(name), name, display_name, dim, dtype, self.device, self.index_factory)
         with self._lock:
             self._stores[name] = st
         return st
 
+    def _evict(self, name):
+        st = self._stores.pop(name, None)
+        if st is not None:
+            st.close()
+        for cb in self.on_evict:
+            cb(name)
+
     def get(self, name):
         with self._lock:
             st = self._stores.get(name)
-            if st is not None and not st.stale():
-                return st
+            if st is not None:
+                if not st.stale():
+                    return st
+                if st.refresh():
+                    return st
+                self._evict(name)  # dropped by another process (cleanup.py delete_store)
+                return None
             d = self._dir(name)
             if d is None or not os.path.exists(os.path.join(d, "manifest.json")):
                 return None
-            st = LocalStore.load(d, self.device)
+            try:
+                st = LocalStore.open(d, self.device, self.index_factory)
+            except StoreGone:
+                return None
             self._stores[name] = st
             return st
 
     def drop(self, name) -> bool:
         with self._lock:
-            st = self._stores.pop(name, None)
-            if st is not None:
-                st.index.close()
+            had = name in self._stores
+            self._evict(name)
             d = self._dir(name)
             if d and os.path.isdir(d):
+                # the manifest goes first: other processes see the store gone, not half-deleted
+                try:
+                    os.unlink(os.path.join(d, "manifest.json"))
+                except FileNotFoundError:
+                    pass
                 shutil.rmtree(d, ignore_errors=True)
                 return True
-            return st is not None
+            return had
 
     def names(self):
         out = set(self._stores)

@@ -87,3 +87,72 @@ class OracleRetriever:
                 hits.append((-sc, si, row, Hit(float(sc), name, int(row), fid, text, title, f"local://{name}/{fid}")))
         hits.sort(key=lambda h: h[:3])
         return [h[3] for h in hits[:k]]
+
+
+class HostIndex:
+    """Test-only host stand-in for rfx.index.DeviceIndex, with the same interface LocalStore
+    uses and the same append-only row-file format as rfx_rows_append / rfx_rows_sync (64-byte
+    header "RFXROWS1", u32 version 1, u32 dim, u32 dtype; row-major rows).  Lets the store's file
+    protocol (commit point, torn tails, cross-process catch-up, writer lock) run on a CPU."""
+
+    CODES = {"f32": (0, np.float32), "bf16": (1, np.uint16), "f16": (2, np.float16)}
+    syncs = []  # (path, rows before, upto) of every rows_sync, for the incremental-load tests
+
+    def __init__(self, dim, dtype="f32", device=0, capacity=0):
+        self.dim, self.dtype, self.device = int(dim), dtype, device
+        self.code, self.np_dtype = self.CODES[dtype]
+        self.data = np.zeros((0, self.dim), dtype=self.np_dtype)
+        self.closed = False
+
+    def _hdr(self):
+        h = bytearray(64)
+        h[:8] = b"RFXROWS1"
+        h[8:20] = np.array([1, self.dim, self.code], dtype="<u4").tobytes()
+        return bytes(h)
+
+    @property
+    def rows(self):
+        return self.data.shape[0]
+
+    def add(self, vecs):
+        v = np.asarray(vecs, dtype=self.np_dtype).reshape(-1, self.dim)
+        first = self.rows
+        self.data = np.concatenate([self.data, v])
+        return first
+
+    def rows_append(self, path, row0):
+        import os
+        fd = os.open(path, os.O_RDWR | os.O_CREAT, 0o644)
+        try:
+            if os.fstat(fd).st_size >= 64:
+                assert os.pread(fd, 64, 0) == self._hdr()
+            else:
+                assert row0 == 0
+                os.pwrite(fd, self._hdr(), 0)
+            rb = self.dim * self.data.itemsize
+            os.ftruncate(fd, 64 + row0 * rb)
+            os.pwrite(fd, self.data[row0:].tobytes(), 64 + row0 * rb)
+            os.fsync(fd)
+        finally:
+            os.close(fd)
+
+    def rows_sync(self, path, upto):
+        HostIndex.syncs.append((path, self.rows, upto))
+        rb = self.dim * self.data.itemsize
+        with open(path, "rb") as f:
+            assert f.read(64) == self._hdr()
+            f.seek(64 + self.rows * rb)
+            raw = f.read((upto - self.rows) * rb)
+        assert len(raw) == (upto - self.rows) * rb, "row file shorter than the committed count"
+        self.data = np.concatenate([self.data, np.frombuffer(raw, dtype=self.np_dtype).reshape(-1, self.dim)])
+
+    def tombstone(self, rows):
+        rows = np.asarray(rows, dtype=np.int64)
+        self.data = self.data.copy()
+        self.data[rows] = np.nan if self.dtype != "bf16" else 0x7FC0
+
+    def mask_tensor(self, words):
+        return words
+
+    def close(self):
+        self.closed = True

@@ -109,3 +109,32 @@ def test_many_rounds_no_deadlock():
 def test_bad_max_batch():
     with pytest.raises(ValueError):
         GroupBatcher(lambda items: items, max_batch=0)
+
+
+def test_waiter_times_out_with_a_retryable_error_and_leaves_the_queue():
+    """A hung launch must not block every chat thread forever: a queued
+    caller gives up after the batcher's timeout with a TimeoutError (retryable, gemini_rag.py:
+    17-27) and is removed from the queue, so the next batch does not run its request."""
+    from rfx.batcher import BatchTimeout
+
+    release = threading.Event()
+    ran = []
+
+    def run(items):
+        ran.append(list(items))
+        if items[0] == "slow":
+            release.wait(5)
+        return list(items)
+
+    b = GroupBatcher(run, timeout=0.2)
+    t = threading.Thread(target=lambda: b.submit("slow"))
+    t.start()
+    time.sleep(0.05)
+    t0 = time.monotonic()
+    with pytest.raises(TimeoutError) as ei:
+        b.submit("waiter")
+    assert isinstance(ei.value, BatchTimeout) and time.monotonic() - t0 < 2
+    release.set()
+    t.join(timeout=5)
+    assert b.submit("after") == "after"
+    assert ["waiter"] not in ran and ran[-1] == ["after"]

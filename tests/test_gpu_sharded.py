@@ -1,0 +1,126 @@
+"""GPU: the row-sharded store behind the drop-in adapter (rfx.sharded.ShardedIndex, RFX_DEVICES)
+and the RCCL communicator inside the C ABI (rfx_comm_* / rfx_allgather_records).
+
+On the one-GPU box the shards are logical (RFX_DEVICES=0x4: four row ranges on cuda:0; the
+exchange is a device-local stack); the RCCL path is exercised by a 1-rank communicator in both
+process models (ncclCommInitRank and ncclCommInitAll).  The 8-GPU run is the driver's."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DOCS = [("alpha beta gamma delta epsilon " * 40, {"tenant": "acme"}),
+        ("zeta eta theta iota kappa lambda " * 35, {"tenant": "globex"}),
+        ("mock mode document assistant retrieval citations " * 30, {"tenant": "acme"}),
+        ("hbm bandwidth roofline matrix cores wavefront lds " * 33, None)]
+QUESTIONS = ["alpha gamma", "theta kappa lambda", "document retrieval", "roofline lds", "beta zeta assistant"]
+
+
+def _hits(ret, name, q, k, filt=None):
+    return [(h.row, h.score, h.file_id) for h in ret.search([name], q, k, metadata_filter=filt)]
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_sharded_adapter_equals_unsharded(tmp_path, dtype):
+    from rfx import store as rstore
+    from rfx.retriever import GpuRetriever
+    from rfx.sharded import ShardedIndex
+
+    root = str(tmp_path)
+    writer = GpuRetriever(registry=rstore.StoreRegistry(root=root, device=0), dtype=dtype)
+    name = writer.create_store("shared")
+    ids = [writer.add_document(name, t, f"doc{i}", {"white_space_config": {"max_tokens_per_chunk": 4}}, m)[0]
+           for i, (t, m) in enumerate(DOCS)]
+    plain = GpuRetriever(registry=rstore.StoreRegistry(root=root, device=0), dtype=dtype)
+    sharded = GpuRetriever(registry=rstore.StoreRegistry(root=root, device=0, devices="0x4"), dtype=dtype)
+    six = sharded.registry.get(name).index
+    assert isinstance(six, ShardedIndex) and len(six.shards) == 4
+    assert min(s.rows for s in six.shards) > 0 and six.rows == plain.registry.get(name).index.rows
+
+    def same():
+        for q in QUESTIONS:
+            for k in (1, 5, 10):
+                assert _hits(sharded, name, q, k) == _hits(plain, name, q, k)
+            assert _hits(sharded, name, q, 7, {"tenant": "acme"}) == _hits(plain, name, q, 7, {"tenant": "acme"})
+
+    same()
+    # growth lands on the last shard; deletions anywhere
+    writer.add_document(name, "nu xi omicron pi rho sigma " * 20, "late", None, {"tenant": "acme"})
+    writer.delete_file(name, ids[1])
+    same()
+    assert sharded.registry.get(name).index.shards[-1].rows > six.shards[0].rows
+
+    # a batched search (MFMA kernels) straight on the indexes: bit-identical rows and scores
+    pst = plain.registry.get(name)
+    emb = plain.embedder(768)
+    qs = emb.embed_texts([f"{w} {v}" for w in ("alpha", "theta", "roofline", "sigma") for v in range(64)], dtype)
+    a_s, a_r = pst.index.search(qs, 10)
+    b_s, b_r = six.search(qs, 10)
+    assert torch.equal(a_r, b_r) and torch.equal(a_s, b_s)
+
+
+def test_sharded_index_split_and_masks(tmp_path):
+    """Shard bases are multiples of 32 (mask words never straddle shards); a masked batched
+    search over 3 logical shards equals the unsharded masked search."""
+    from rfx import filters
+    from rfx.index import DeviceIndex
+    from rfx.sharded import ShardedIndex
+
+    n = 10_007
+    whole = DeviceIndex(768, "bf16", 0)
+    whole.add_synthetic(3, n)
+    path = str(tmp_path / "rows.rfx")
+    whole.rows_append(path, 0)
+    sh = ShardedIndex(768, "bf16", [0, 0, 0])
+    sh.rows_sync(path, n)
+    assert all(b % 32 == 0 for b in sh.bases) and sh.rows == n
+    words = filters.row_mask_words(n, [(5, 3000), (4100, 10), (9000, 1007)])
+    q = whole.read(0, 300)[::3].contiguous()  # 100 queries
+    m_whole = torch.from_numpy(words).cuda()
+    a = whole.search(q, 10, row_mask=m_whole)
+    b = sh.search(q, 10, row_mask=sh.mask_tensor(words))
+    assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0])
+    sh.tombstone([6, 9000, 4105])
+    whole.tombstone([6, 9000, 4105])
+    a = whole.search(q[:5], 10)
+    b = sh.search(q[:5], 10)
+    assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0])
+
+
+def _records(nq, k, seed):
+    g = torch.Generator().manual_seed(seed)
+    s = torch.rand((nq, k), generator=g).sort(dim=1, descending=True).values
+    r = torch.randint(0, 1 << 40, (nq, k), generator=g)
+    from rfx.dist import pack
+    return pack(s, r).cuda()
+
+
+def test_rccl_rank_communicator_one_rank():
+    from rfx.dist import RcclComm, gather_merge_records
+
+    comm = RcclComm.for_rank(1, 0, 0, RcclComm.unique_id())
+    assert (comm.world, comm.rank, comm.n_local) == (1, 0, 1)
+    rec = _records(256, 10, 1)
+    out = torch.empty((1, 256, 10, 2), dtype=torch.int64, device="cuda")
+    st = torch.cuda.current_stream()
+    comm.allgather_records([rec], [out], [st])
+    torch.cuda.synchronize()
+    assert torch.equal(out[0], rec)
+    s, r = gather_merge_records(rec, 10, comm=comm)
+    assert torch.equal(r.cpu(), rec[..., 1].cpu())
+    assert np.array_equal(s.cpu().numpy().view(np.int32), rec[..., 0].cpu().numpy().astype(np.int32))
+    comm.close()
+
+
+def test_rccl_group_communicator_one_device():
+    from rfx.dist import RcclComm
+
+    comm = RcclComm.for_devices([0])
+    assert (comm.world, comm.n_local) == (1, 1)
+    rec = _records(3, 5, 2)
+    out = torch.zeros((1, 3, 5, 2), dtype=torch.int64, device="cuda")
+    comm.allgather_records([rec], [out], [torch.cuda.current_stream()])
+    torch.cuda.synchronize()
+    assert torch.equal(out[0], rec)
+    comm.close()
