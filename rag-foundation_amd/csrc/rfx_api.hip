@@ -561,6 +561,8 @@ int rfx_rows_append(rfx_index_t h, const char* path, int64_t row0, int64_t file_
     return fail(RFX_EIO, "%s holds no rows, cannot append at row %lld", path, (long long)(file_base + row0));
   } else if (pwrite(f.fd, want, kRowsHdr, 0) != kRowsHdr) {
     return fail(RFX_EIO, "header write to %s failed", path);
+  } else {
+    sb.st_size = kRowsHdr;
   }
   const int64_t rb = ix->row_bytes();
   const off_t at = kRowsHdr + (file_base + row0) * rb;

@@ -130,6 +130,7 @@ class HostIndex:
                 assert row0 == 0
                 os.pwrite(fd, self._hdr(), 0)
             rb = self.dim * self.data.itemsize
+            assert os.fstat(fd).st_size >= 64 + row0 * rb, "row file shorter than the append point"
             os.ftruncate(fd, 64 + row0 * rb)
             os.pwrite(fd, self.data[row0:].tobytes(), 64 + row0 * rb)
             os.fsync(fd)
