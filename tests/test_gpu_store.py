@@ -83,8 +83,10 @@ def test_delete_visible_to_other_process_view(tmp_path):
     rstore.set_registry(rstore.StoreRegistry(root=root, device=0))
     ret = GpuRetriever(dtype="f32")
     name = ret.create_store("s")
-    fa, _ = ret.add_document(name, "alpha beta gamma delta", "a", {"white_space_config": {"max_tokens_per_chunk": 2}})
-    ret.add_document(name, "epsilon zeta eta theta", "b", {"white_space_config": {"max_tokens_per_chunk": 2}})
+    fa, _ = ret.add_document(name, "alpha beta gamma delta", "a", {"white_space_config": {"max_tokens_per_chunk": 2,
+                                                                                          "max_overlap_tokens": 0}})
+    ret.add_document(name, "epsilon zeta eta theta", "b", {"white_space_config": {"max_tokens_per_chunk": 2,
+                                                                                  "max_overlap_tokens": 0}})
     other = rstore.StoreRegistry(root=root, device=0)
     assert other.get(name).index.live_rows == 4
     assert ret.delete_file(name, fa)

@@ -8,7 +8,7 @@ mkdir -p "$O"
 cd "$R" || exit 1
 export PYTHONDONTWRITEBYTECODE=1
 echo "== pytest $(date +%T)"
-timeout -k 10 1000 python -u -m pytest tests -m gpu --maxfail=8 -v --timeout 420 --timeout-method thread > "$O/pytest_gpu.log" 2>&1 || { tail -60 "$O/pytest_gpu.log"; exit 1; }
+timeout -k 10 1000 python -u -m pytest ${TESTS:-tests} -m gpu --maxfail=8 -v --timeout 420 --timeout-method thread > "$O/pytest_gpu.log" 2>&1 || { tail -60 "$O/pytest_gpu.log"; exit 1; }
 tail -2 "$O/pytest_gpu.log"
 echo "== rehearsal $(date +%T)"
 run() {
