@@ -4,8 +4,16 @@ local-GPU adapter's outputs have the reference structure.
   MockGeminiRag._mock_response        gemini_rag.py:704-718
   MockGeminiRag.ask_stream (2 chunks)  gemini_rag.py:673-694
   GeminiRag.extract_citations_...      gemini_rag.py:554-595
-Pinned by tests/golden/ref_mock.json, captured from the reference in the build container.
+  chat._citation_frames / _finish_frame chat.py:576-603 (the SSE payloads the chat route builds
+                                        from the adapter's citations and usage)
+Pinning: extract_citations, citation_frame_payloads and finish_frame_payload are checked against
+the reference's own test vectors (tests/golden/ref_boundary.json, extracted from
+backend/tests/test_gemini_rag.py and backend/tests/test_chat_stream_helpers.py by
+tests/golden/make_ref_boundary.py).  mock_response / first_stream_text follow the reference source
+(SURVEY §8c lists the mock's outputs); no reference test calls MockGeminiRag, so those two are
+restated from the source only.
 """
+import json
 from types import SimpleNamespace
 
 
@@ -44,3 +52,21 @@ def extract_citations(response):
         return out
     except (AttributeError, KeyError, IndexError, TypeError):
         return out
+
+
+def citation_frame_payloads(citations):
+    """chat._citation_frames (chat.py:576-586): one "source-document" payload per citation."""
+    return [{"type": "source-document", "sourceId": f"cit-{c['index']}", "mediaType": "file",
+             "title": c.get("title") or c.get("uri") or "Source", "snippet": c.get("snippet")} for c in citations]
+
+
+def citation_frames(citations):
+    """The SSE frames themselves ("data: <json>\n\n")."""
+    return [f"data: {json.dumps(p)}\n\n" for p in citation_frame_payloads(citations)]
+
+
+def finish_frame_payload(*, prompt_tokens, completion_tokens, model):
+    """chat._finish_frame (chat.py:589-603)."""
+    return {"type": "finish", "finishReason": "stop", "promptTokens": prompt_tokens,
+            "completionTokens": completion_tokens,
+            "usage": {"prompt_tokens": prompt_tokens, "completion_tokens": completion_tokens, "model": model}}

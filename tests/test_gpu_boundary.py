@@ -1,0 +1,43 @@
+"""GPU: LocalGpuRag (HIP path) on the config-1 store, k = 1 and k = 5, against the reference's own
+boundary vectors (tests/golden/ref_boundary.json): the citations it yields become chat-route
+payloads (oracle.mock_ref restatement of chat.py:576-603, pinned by the reference's test) with
+exactly the reference payload's shape, in rank order, carrying the oracle's top-k rows
+(tests/golden/cfg1_sample_report.json)."""
+import json
+import os
+
+import pytest
+
+from oracle import mock_ref
+from test_boundary_golden import payload_shape_ok
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_cfg1_frames_k1_k5(golden_dir, tmp_path, dtype):
+    from rfx import store as rstore
+    from rfx.adapter import LocalGpuRag
+    from rfx.retriever import GpuRetriever
+
+    gold = json.load(open(os.path.join(golden_dir, "ref_boundary.json")))
+    fx = json.load(open(os.path.join(golden_dir, "cfg1_sample_report.json")))
+    rstore.set_registry(rstore.StoreRegistry(root=str(tmp_path), device=0))
+    rag = LocalGpuRag(GpuRetriever(dtype=dtype))
+    st = rag.create_store("demo")
+    rag.upload_file(st, os.path.join(golden_dir, "sample_report.md"), display_name="sample-report.md",
+                    chunking_config={"white_space_config": fx["chunking"]})
+    for case in fx["queries"]:
+        for k in (1, 5):
+            chunks = list(rag.ask_stream(contents=[{"role": "user", "parts": [{"text": case["question"]}]}],
+                                         store_names=[st], metadata_filter=None, model="gemini-2.5-flash", top_k=k))
+            assert chunks[0].text == mock_ref.first_stream_text(case["question"])
+            cits = rag.extract_citations_from_response(chunks[1])
+            gc = chunks[1].candidates[0].grounding_metadata.grounding_chunks
+            if dtype == "f32":  # the fixture's oracle rows are for the f32 store
+                assert [g.retrieved_context.row for g in gc] == case["rows"][:k]
+            assert [c["snippet"] for c in cits] == [g.retrieved_context.text for g in gc]
+            payload_shape_ok(mock_ref.citation_frame_payloads(cits), gold["citation_frame"]["payload"],
+                             ["sample-report.md"] * k, [g.retrieved_context.text for g in gc])
+            assert all(c["store"] == st for c in cits)
+    rag.delete_store(st)
