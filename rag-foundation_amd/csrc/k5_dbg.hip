@@ -47,6 +47,9 @@ int launch_scan_mfma5_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
     RFX_K5_DBG(131073)
     RFX_K5_DBG(131081)
     RFX_K5_DBG(262153)
+    RFX_K5_DBG(262144)
+    RFX_K5_DBG(393216)
+    RFX_K5_DBG(393225)
     RFX_K5_DBG(524288)
     RFX_K5_DBG(1048576)
     RFX_K5_DBG(257)

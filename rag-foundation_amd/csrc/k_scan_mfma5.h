@@ -344,20 +344,19 @@ __global__ __launch_bounds__(512, 1) void scan_mfma5_kernel(const uint16_t* __re
 
     // ---- epilogue: fold this tile's 32 rows into the lane list ----
     if constexpr (S16 && (MODE & 2) == 0) {
-      // pair swap, in place: lane (n, g) holds rows 16 rb + 4 g + i of queries n (qb 0) and 16 + n
-      // (qb 1).  Lanes of even g keep query block 0, odd g block 1, and trade the other block with
-      // lane l ^ 16 (g ^ 1).  Afterwards acc4[2 rb + gg][i] is row 16 rb + 8 half + 4 gg + i of the
-      // lane's one query: flat value rb*8 + gg*4 + i (fold's ROWMAP 1).
-      const bool p = (lane >> 4) & 1;
+      // pair swap, in place, one v_permlane16_swap per register pair: lane (n, g) holds rows
+      // 16 rb + 4 g + i of queries n (qb 0) and 16 + n (qb 1).  The swap trades the odd 16-lane rows
+      // of the qb-0 register with the even rows of the qb-1 register, so afterwards a lane of even
+      // g holds query n and one of odd g query 16 + n, acc4[2 rb + gg][i] being row
+      // 16 rb + 8 (g >> 1) + 4 gg + i: flat value rb*8 + gg*4 + i (fold's ROWMAP 1).
 #pragma unroll
       for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float recv = __shfl_xor(p ? acc4[2 * rb][i] : acc4[2 * rb + 1][i], 16);
-          if (p)
-            acc4[2 * rb][i] = recv;
-          else
-            acc4[2 * rb + 1][i] = recv;
+          const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc4[2 * rb][i]),
+                                                          __float_as_uint(acc4[2 * rb + 1][i]), false, false);
+          acc4[2 * rb][i] = __uint_as_float(r[0]);
+          acc4[2 * rb + 1][i] = __uint_as_float(r[1]);
         }
     }
     if constexpr ((MODE & 1) == 0) {
