@@ -207,13 +207,14 @@ def main():
                    "exchange": ("RCCL all-gather from librfx (rfx_allgather_records)" if comm is not None else
                                 "host (gloo) rehearsal" if world > 1 else "none (one shard)"),
                    "scan_kernel": {0: "valu", 1: "mfma128", 2: "mfma256", 3: "mfma_qstationary128",
-                                   4: "mfma_qstationary256", 5: "mfma_qstationary256_2wps"}[kern]},
+                                   4: "mfma_qstationary256", 5: "mfma_qstationary256_2wps",
+                                   6: "mfma16_qstationary256_2wps"}[kern]},
         "achieved_hbm_gbps_per_gpu": round(achieved, 1),
         "build_id": _lib.BUILD_ID,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": load_pmc_traffic(workload_key),
                      "kernel": {0: "scan_valu_kernel", 1: "scan_mfma_kernel", 2: "scan_mfma2_kernel", 3: "scan_mfma3_kernel",
-                                4: "scan_mfma4_kernel", 5: "scan_mfma5_kernel"}[kern],
+                                4: "scan_mfma4_kernel", 5: "scan_mfma5_kernel", 6: "scan_mfma6_kernel"}[kern],
                      "kernel_ms": round(scan_ms, 4), "alg_bytes_per_launch": alg_bytes},
     }
 

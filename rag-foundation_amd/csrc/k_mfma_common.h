@@ -100,6 +100,12 @@ __device__ __forceinline__ void glds_sc1(const void* src, uint32_t lds_addr) {
                : "memory", "m0");
 }
 
+// 16 values of four 16x16 accumulators as one flat vector (no copies)
+struct Acc4View {
+  const v4f32x4 (&a)[4];
+  __device__ __forceinline__ float operator[](int r) const { return a[r >> 2][r & 3]; }
+};
+
 // min over the first KL threshold slots of one query (LDS image [q][kTauW] u32, 48 B per query)
 template <int KL>
 __device__ __forceinline__ uint32_t tau_min(const uint8_t* p) {

@@ -47,11 +47,7 @@ using mfc::tau_min;
 using mfc::unord;
 using mfc::v4f32x16;
 
-// 16 values of four 16x16 accumulators as one flat vector (no copies)
-struct Acc4View {
-  const v4f32x4 (&a)[4];
-  __device__ __forceinline__ float operator[](int r) const { return a[r >> 2][r & 3]; }
-};
+using mfc::Acc4View;
 
 constexpr int kWaves = 8;
 constexpr int kTM = 32;                   // rows per tile

@@ -1,0 +1,301 @@
+// k_scan_mfma6.h — the headline scan (BASELINE config 3: 10M×768 bf16, nq 256, k 10): all-query-
+// stationary, two waves per SIMD, v_mfma_f32_16x16x32, corpus stream by LDS-DMA into an LDS image
+// whose fragment reads need no per-read address arithmetic.
+//
+// Path: the retrieval half of GeminiRag.ask_stream (backend/app/services/gemini_rag.py:517-551).
+// Fused scan + per-query top-k; the score matrix never reaches HBM.
+//
+// What changed against k_scan_mfma5.h (its ablations: tools/k5_variants.py, profiles/r02_*):
+//   * MFMA shape 16x16x32 (2 row blocks × 2 query blocks per 32-deep k-step): same MFMA cycles and
+//     LDS bytes per FLOP as 32x32x16, and the chip holds a higher clock on it (MI355X_MICROARCH.md
+//     'DVFS give-back' item 7); measured -2.4 % on kernel 5.  The epilogue's query-pair swap is one
+//     v_permlane16_swap per register pair.
+//   * LDS image [8-row group][16-B chunk][row]: chunk c of row r of a stage slot at byte
+//     (r >> 3) * 4096 + c * 128 + (r & 7) * 16.  A lane's fragment for (row block rb, k-step kk)
+//     sits at a fixed per-lane base + rb * 8192 + kk * 512, so every ds_read_b128 takes its address
+//     from one base register and an immediate offset (kernel 5's XOR swizzle cost one v_add and one
+//     held offset register per k-step, and the kernel spilled).  The 16-lane groups of each read hit
+//     16 distinct bank quads (conflict-free).
+//   * An LDS-DMA piece (1 KB) is 8 rows × 128 B — whole 128-B lines of the corpus — and lands as
+//     one contiguous KB of the image: piece i = rows 8 (i >> 2) .. +7, chunks 8 (i & 3) .. +7.
+// Everything else as kernel 5: workgroup = 8 waves × 32 resident queries (192 VGPRs of B
+// fragments); 32-row tiles, block b takes tiles b, b + B, ...; a stage = 32 rows × 256 dims
+// (16 KB) in a 6-slot ring, 5 stages in flight, one counted vmcnt + s_barrier per stage; per-lane
+// sorted top-KL lists in LDS behind a pruning bound shared across workgroups through a per-query
+// slot table (k_mfma_common.h fold / tau_min).
+// Requires the index invariant of rfx_api.hip: rows [nrows, capacity) are NaN and capacity is a
+// multiple of 128, so the ragged last tile needs no clamping or masking.
+// Algorithmic bytes per tile: 32 * D * esize.
+#pragma once
+#include "k_mfma_common.h"
+
+namespace rfx {
+namespace k6 {
+
+using namespace mfc;
+
+constexpr int kWaves = 8;
+constexpr int kTM = 32;                   // rows per tile
+constexpr int kQW = 32;                   // queries per wave
+constexpr int kQG = kWaves * kQW;         // 256 queries per workgroup
+constexpr int kSK = 256;                  // dims per stage
+constexpr int kSlot = kTM * kSK * 2;      // 16 KB
+constexpr int kRing = 6;                  // 5 stages (80 KB) in flight
+constexpr int kGPW = 2;                   // LDS-DMA pieces per wave per stage (16 KB / 1 KB / 8 waves)
+constexpr int kTauW = 16;                 // u32 per query in the threshold table (KL <= 10 used)
+constexpr int kTauOff = kRing * kSlot;    // 96 KB
+constexpr int kTauBytes = kQG * kTauW * 4;  // 16 KB: 16 DMA pieces, 2 per wave
+constexpr int kTauGPW = kTauBytes / 1024 / kWaves;
+constexpr int kListOff = kTauOff + kTauBytes;
+template <int KL>
+constexpr int lds_bytes() { return kListOff + kWaves * KL * 64 * 8; }  // + lane lists [wave][KL][64] u64
+static_assert(lds_bytes<10>() <= 163840, "LDS budget");
+static_assert(kSlot / 1024 == kWaves * kGPW && kTauGPW == 2, "DMA pieces per wave");
+
+// Threshold-table refreshes go out after the last stage of tiles 0, 1, 3, 7, 11, ... (the lists
+// start empty, so the first tiles take the slow insert path until the slot table's bound arrives;
+// then every 4 tiles: a staler bound sends more lanes into the insert path — kernel 5 ablations).
+__device__ __forceinline__ bool tau_refresh_tile(int it) { return it < 2 || (it & 3) == 3; }
+
+// Metadata filter: row bit of the lane's value r after the epilogue's pair swap (fold ROWMAP 1,
+// bits pre-shifted by 8 * half): (r & 7) + 16 * (r >> 3).
+template <class V>
+__device__ __forceinline__ void mask_rowmap1(V& a, uint32_t bits) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r)
+    if (!((bits >> ((r & 7) + 16 * (r >> 3))) & 1u)) a[r >> 2][r & 3] = __builtin_nanf("");
+}
+
+// MODE: 0 production; kModeMask = row-masked variant (metadata filter); debug-build ablations:
+// 1 = no top-k epilogue (MFMAs kept live), 8 = no corpus stream after the prologue.
+constexpr int kModeMask = 2097152;
+
+template <int DT, int KL, int D, int MODE = 0>
+__global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Qp,
+                                                            int nq, int ntiles, uint32_t* __restrict__ tau,
+                                                            float* __restrict__ cand_s, int* __restrict__ cand_r,
+                                                            int64_t n_lists, const uint32_t* __restrict__ mask) {
+  constexpr int NKS = D / 32;   // 32-deep k-steps per tile
+  constexpr int NST = D / kSK;  // stages per tile
+  constexpr int KPS = kSK / 32;  // k-steps per stage (8)
+  static_assert(D % kSK == 0, "D must be a multiple of 256");
+  static_assert(KL <= 10, "threshold table holds 10 slots");
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[lds_bytes<KL>()];
+
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, lane = tid & 63;
+  const int half = lane >> 5;
+  const int range = blockIdx.x;
+  const int qg = blockIdx.y * kQG;
+  // this lane's query after the epilogue's pair swap: lanes of odd 16-lane row hold query block 1
+  const int q = qg + w * kQW + 16 * ((lane >> 4) & 1) + (lane & 15);
+  const int nblk = gridDim.x;
+  const int nt = range < ntiles ? (ntiles - range + nblk - 1) / nblk : 0;
+  const int S = nt * NST;
+  if (S == 0) return;  // (cannot happen with the host plan; whole workgroup exits together)
+  const int lst = range * 2 + half;  // this lane's list id (per query)
+
+  // ---- LDS init: threshold image and lane lists start at 0 (= "no bound" / empty) ----
+  {
+    uint4* tz = (uint4*)(lds + kTauOff);
+#pragma unroll
+    for (int i = 0; i < kTauBytes / 16 / 512; ++i) tz[tid + 512 * i] = uint4{0u, 0u, 0u, 0u};
+  }
+  uint64_t* const Ls = (uint64_t*)(lds + kListOff) + (w * KL) * 64 + lane;
+#pragma unroll
+  for (int i = 0; i < KL; ++i) Ls[i * 64] = 0ull;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // no LDS-DMA in flight yet: a plain barrier
+
+  // ---- resident query fragments (B[k][col] of 16x16x32): query block qb, lane holds col
+  // 16 qb + (lane & 15), k = 32 ks + 8 (lane >> 4) + j
+  uint4 bq[2 * NKS];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const uint16_t* qa = Qp + (int64_t)(qg + w * kQW + 16 * qb + (lane & 15)) * D + 8 * (lane >> 4);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) bq[2 * ks + qb] = *(const uint4*)(qa + 32 * ks);
+  }
+
+  // ---- LDS-DMA pieces: piece i = w + 8 u (u = 0, 1) of a stage = rows 8 (i >> 2) + (lane & 7),
+  // chunks 8 (i & 3) + (lane >> 3): 8 rows × 128 B, one contiguous KB of the slot image
+  uint32_t laneoff[kGPW];  // byte offset of this lane's 16 B inside a [32 rows][D] tile (stage 0)
+#pragma unroll
+  for (int u = 0; u < kGPW; ++u) {
+    const int i = w + kWaves * u;
+    laneoff[u] = (uint32_t)((8 * (i >> 2) + (lane & 7)) * D + (8 * (i & 3) + (lane >> 3)) * 8) * 2u;
+  }
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
+  const int64_t tile_stride = (int64_t)nblk * kTM * D;  // elements between a block's tiles
+  // piece u of stage gi -> LDS slot `slot`.  gi is clamped to the last stage so the tail of the
+  // stream issues harmless duplicate loads into free slots: every stage issues exactly kGPW
+  // LDS-DMA ops per wave and the counted waits stay exact.
+  auto issue_piece = [&](int gi, int slot, int u) {
+    gi = gi < S ? gi : S - 1;
+    const int ti = gi / NST;
+    const int si = gi - ti * NST;
+    const uint16_t* tbase = X + (int64_t)range * kTM * D + ti * tile_stride + si * kSK;
+    bdma(make_rsrc(tbase), laneoff[u],
+         __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)(slot * kSlot) + (uint32_t)((w + kWaves * u) * 1024)));
+  };
+  const v4i32 tau_rsrc = make_rsrc(tau);
+  auto issue_tau = [&]() {
+#pragma unroll
+    for (int u = 0; u < kTauGPW; ++u) {
+      const int i = w + kWaves * u;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + kTauOff + i * 1024);
+      bdma_sc1(tau_rsrc, (uint32_t)(qg * kTauW * 4 + tid * 16 + u * kWaves * 1024), dst);
+    }
+  };
+
+  uint32_t thr = 0u;  // pruning bound (orderable score; 0 = none)
+  const uint32_t slot_voff = (uint32_t)(q * kTauW + lst % KL) * 4u;
+  const uint8_t* const tq = lds + kTauOff + (w * kQW + (lane & 15) + 16 * ((lane >> 4) & 1)) * (kTauW * 4);
+  int n_slow = 0;  // (fold's diagnostic counter; unused here)
+  // A fragment of row block rb, k-step kk of a slot: per-lane base + rb * 8192 + kk * 512
+  const uint8_t* const frag_base = lds + ((lane >> 3) & 1) * 4096 + (lane >> 4) * 128 + (lane & 7) * 16;
+  struct Frag {
+    uint4 a[2];
+  };
+  auto read_frag = [&](int slot, int kk) -> Frag {
+    const uint8_t* p = frag_base + slot * kSlot + kk * 512;
+    Frag f;
+    f.a[0] = *(const uint4*)p;
+    f.a[1] = *(const uint4*)(p + 8192);
+    return f;
+  };
+
+  // Schedule.  Stage h's pieces go out during stage h - 5, at k-steps 0 and 4, into the slot freed
+  // at stage h - 6's barrier.  Fragments are read one k-step ahead of their MFMAs; the stage-end
+  // wait + barrier sit at k-step KPS - 1, once every wave has issued (and, by lgkmcnt(0), received)
+  // its last read of the stage.
+  constexpr int PF = 1;
+  constexpr int NF = PF + 1;
+  constexpr int KB = KPS - PF;
+  constexpr int AHEAD = kRing - 1;
+  constexpr int YNG = (kRing - 2) * kGPW;  // ops younger than the next stage (8)
+  static_assert((NST * KPS) % NF == 0, "fragment rotation must realign every tile");
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // resident queries landed before the counted stream
+  issue_tau();
+#pragma unroll
+  for (int p = 0; p < AHEAD; ++p)
+#pragma unroll
+    for (int u = 0; u < kGPW; ++u) issue_piece(p, p, u);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(YNG) : "memory");  // stage 0 landed: stages 1..4 younger
+  asm volatile("s_barrier" ::: "memory");
+
+  Frag fr[NF];
+  fr[0] = read_frag(0, 0);
+  v4f32x4 acc4[4];  // [rb * 2 + qb]
+  for (int it = 0; it < nt; ++it) {
+    const int tile = range + it * nblk;
+    const int gbase = it * NST;
+    if constexpr ((MODE & 1) == 0)  // refreshed threshold image (issued 2 tiles ago; any value is a valid bound)
+      if (it >= 2 && tau_refresh_tile(it - 2)) thr = max(thr, tau_min<KL>(tq));
+    // A threshold refresh (kTauGPW ops) issued after the barrier of stage g_r = last stage of a
+    // refresh tile it_r is younger than stage g+1's pieces iff g-4 <= g_r <= g-1: at every stage of
+    // tile it_r + 1 and at stage 0 of tile it_r + 2 (overlaps admit one: stricter, never looser).
+    const bool tau_young12 = it >= 1 && tau_refresh_tile(it - 1);
+    const bool tau_young0 = tau_young12 || (it >= 2 && tau_refresh_tile(it - 2));
+#pragma unroll
+    for (int s = 0; s < NST; ++s) {
+      const int g = gbase + s;
+      const int slot = g % kRing;
+#pragma unroll
+      for (int kk = 0; kk < KPS; ++kk) {
+        if constexpr ((MODE & 8) == 0)
+          if (kk % (KPS / kGPW) == 0) issue_piece(g + kRing - 1, (g + kRing - 1) % kRing, kk / (KPS / kGPW));
+        if (kk == KB) {
+          // stage g+1 landed for this wave: ops younger than its pieces = stages g+2..g+5 (8)
+          // [+ a threshold refresh (2)]; lgkmcnt(0) + barrier: every wave has received its last
+          // fragment of slot g, which may be refilled from here on.
+          if constexpr ((MODE & 8) == 0) {
+            if (s == 0 ? tau_young0 : tau_young12)
+              asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(YNG + kTauGPW) : "memory");
+            else
+              asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(YNG) : "memory");
+          } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          }
+          asm volatile("s_barrier" ::: "memory");
+          if constexpr ((MODE & 8) == 0)
+            if (s == NST - 1 && tau_refresh_tile(it)) issue_tau();
+        }
+        const int ks = s * KPS + kk;
+        // prefetch k-step kk + 1 (crossing into stage g+1 after the barrier)
+        fr[(ks + PF) % NF] = kk + PF < KPS ? read_frag(slot, kk + PF) : read_frag((g + 1) % kRing, kk + PF - KPS);
+        const Frag& cur = fr[ks % NF];
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // the prefetch reads go out first
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb)
+            acc4[2 * rb + qb] = ks == 0 ? mfma16<DT>(cur.a[rb], bq[2 * ks + qb], v4f32x4{})
+                                        : mfma16<DT>(cur.a[rb], bq[2 * ks + qb], acc4[2 * rb + qb]);
+      }
+    }
+
+    // ---- epilogue: pair swap (lane of even 16-lane row g keeps query n, odd keeps 16 + n; one
+    // v_permlane16_swap per register pair), then fold the lane's 16 rows into its list
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc4[2 * rb][i]),
+                                                        __float_as_uint(acc4[2 * rb + 1][i]), false, false);
+        acc4[2 * rb][i] = __uint_as_float(r[0]);
+        acc4[2 * rb + 1][i] = __uint_as_float(r[1]);
+      }
+    if constexpr ((MODE & 1) == 0) {
+      if constexpr ((MODE & kModeMask) != 0) mask_rowmap1(acc4, mask[tile] >> (8 * half));
+      fold<KL, 1>(Acc4View{acc4}, Ls, thr, tile * kTM + 8 * half, tau_rsrc, slot_voff, n_slow);
+    } else {
+      if (acc4[0][0] == 12345.f && acc4[1][1] == 54321.f && acc4[2][2] == 1.f && acc4[3][3] == 2.f) Ls[0] = 1;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (q < nq) {
+    // Drop entries below the query's bound as it stands now, read fresh from the slot table (all
+    // workgroups end together, so it is close to final): valid bound => exact, and the merge then
+    // sees ~k live candidates per query instead of 512 lists.
+    uint32_t m = 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < KL; ++j)
+      m = min(m, __hip_atomic_load(tau + (int64_t)q * kTauW + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const uint32_t fin = max(thr, m);
+    const int64_t o = ((int64_t)q * n_lists + lst) * KL;
+#pragma unroll
+    for (int i = 0; i < KL; ++i) {
+      const uint64_t key = Ls[i * 64];
+      const bool keep = key && (uint32_t)(key >> 32) >= fin;
+      cand_s[o + i] = keep ? unord((uint32_t)(key >> 32)) : -__builtin_inff();
+      cand_r[o + i] = keep ? (int)(~(uint32_t)key) : kEmptyRow;
+    }
+  }
+}
+
+// one translation unit per (dtype, D) instantiates the kernel for the lane-list sizes KL in {4, 10}
+#define RFX_K6_INSTANTIATE(DTV, DV, NAME)                                                                  \
+  int NAME(int kl, dim3 grid, hipStream_t st, const uint16_t* X, const uint16_t* Qp, int nq, int ntiles,     \
+           uint32_t* tau, float* cs, int* cr, int64_t n_lists, const uint32_t* mask) {                      \
+    if (kl == 4 && !mask)                                                                                \
+      hipLaunchKernelGGL((scan_mfma6_kernel<DTV, 4, DV>), grid, dim3(512), 0, st, X, Qp, nq, ntiles, tau, cs, \
+                         cr, n_lists, mask);                                                              \
+    else if (kl == 10 && !mask)                                                                          \
+      hipLaunchKernelGGL((scan_mfma6_kernel<DTV, 10, DV>), grid, dim3(512), 0, st, X, Qp, nq, ntiles, tau,  \
+                         cs, cr, n_lists, mask);                                                          \
+    else if (kl == 4)                                                                                    \
+      hipLaunchKernelGGL((scan_mfma6_kernel<DTV, 4, DV, kModeMask>), grid, dim3(512), 0, st, X, Qp, nq,     \
+                         ntiles, tau, cs, cr, n_lists, mask);                                             \
+    else if (kl == 10)                                                                                   \
+      hipLaunchKernelGGL((scan_mfma6_kernel<DTV, 10, DV, kModeMask>), grid, dim3(512), 0, st, X, Qp, nq,    \
+                         ntiles, tau, cs, cr, n_lists, mask);                                             \
+    else                                                                                                 \
+      return -1;                                                                                         \
+    return 0;                                                                                            \
+  }
+
+}  // namespace k6
+}  // namespace rfx

@@ -144,8 +144,8 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
   L.kernel = 0;
   if (nq > 8) {
     if (nq > 128) {
-      L.mp = rfx::plan_scan_mfma5(ix.rows, ix.dim, ix.dtype, nq, k);
-      if (L.mp.ok) L.kernel = 5;
+      L.mp = rfx::plan_scan_mfma6(ix.rows, ix.dim, ix.dtype, nq, k);
+      if (L.mp.ok) L.kernel = 6;
     }
     if (L.kernel == 0 && nq > 64) {
       L.mp = rfx::plan_scan_mfma3(ix.rows, ix.dim, ix.dtype, nq, k);
@@ -164,8 +164,8 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
   if (L.kernel) {
     L.n_cand = L.mp.n_lists * L.mp.k_lane;
     L.q_bytes = (size_t)L.mp.nq_pad * ix.dim * 2;
-    if (L.kernel == 5)
-      tau_bytes = rfx::tau_bytes_mfma5(L.mp);
+    if (L.kernel == 6)  // (>= kernel 5's table: the debug build runs either on this layout)
+      tau_bytes = std::max(rfx::tau_bytes_mfma6(L.mp), rfx::tau_bytes_mfma5(L.mp));
     else if (L.kernel >= 2)
       tau_bytes = (size_t)(L.mp.nq_pad + 256) * 4;  // + slack: 1 KB threshold DMA per group
   } else {
@@ -248,7 +248,8 @@ int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq,
     rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, 2, qpad, st);
     uint32_t* tau = (uint32_t*)(ws + L.tau_off);
     const int rc =
-        L.kernel == 5 ? rfx::launch_scan_mfma5(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
+        L.kernel == 6 ? rfx::launch_scan_mfma6(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
+        : L.kernel == 5 ? rfx::launch_scan_mfma5(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
         : L.kernel == 3 ? rfx::launch_scan_mfma3(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
         : L.kernel == 2 ? rfx::launch_scan_mfma2(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
                         : rfx::launch_scan_mfma(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, cs, cr, st, mask);
@@ -771,7 +772,10 @@ int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k
   void* qpad = (uint8_t*)ws_d + L.q_off;
   rfx::launch_pad_queries(queries_d, nq, L.mp.nq_pad, ix->dim, 2, qpad, st);
   int rc2;
-  if (mode >= 1000 && mode < 16000000)  // two-waves-per-SIMD kernel ablations: mode 1000 + MODE
+  if (mode >= 20000000)  // headline kernel (k_scan_mfma6.h) ablations: mode 20000000 + MODE
+    rc2 = rfx::launch_scan_mfma6_dbg(rfx::plan_scan_mfma6(ix->rows, ix->dim, ix->dtype, nq, k), mode - 20000000, ix->data,
+                                     (int)ix->rows, ix->dtype, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st);
+  else if (mode >= 1000 && mode < 16000000)  // kernel-5 ablations: mode 1000 + MODE
     rc2 = rfx::launch_scan_mfma5_dbg(rfx::plan_scan_mfma5(ix->rows, ix->dim, ix->dtype, nq, k), mode - 1000, ix->data,
                                      (int)ix->rows, ix->dtype, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st);
   else if (mode >= 20 && mode < 1000)  // all-query-stationary kernel ablations: mode 20 + MODE

@@ -57,7 +57,7 @@ def test_cfg3_fullsize_headline_kernel(rindex):
     ix = rindex.DeviceIndex(768, "bf16", 0, capacity=n)
     ix.add_synthetic(0, n)  # bench.py's corpus (seed 0) and queries (seed 1)
     q = rindex.synth_rows(1, 0, nq, 768, "bf16")
-    assert ix.plan(nq, k)[0] == 5, "cfg3 must run the headline kernel"
+    assert ix.plan(nq, k)[0] == 6, "cfg3 must run the headline kernel"
     s, r = ix.search(q, k)
     torch.cuda.synchronize()
     oracle_check(ix, n, q, s, r, k)

@@ -193,10 +193,10 @@ def test_search_tombstones(rfx):
 
 # ---- search: MFMA path (batched bf16/f16) ----------------------------------------------------------
 def expected_mfma_kernel(nq, k, dim):
-    """Mirror of make_layout (rfx_api.hip): 5 = 256-query-stationary, 2 waves/SIMD (d 768, k <= 10, nq > 128),
+    """Mirror of make_layout (rfx_api.hip): 6 = 256-query-stationary, 2 waves/SIMD (d 768, k <= 10, nq > 128),
     3 = 128-query-stationary (d 768/1024, k <= 16, nq > 64), 2 = 256x256 tiles, 1 = 64-query tiles."""
     if nq > 128 and dim == 768 and k <= 10:
-        return 5
+        return 6
     if nq > 64 and dim in (768, 1024) and k <= 16:
         return 3
     if nq > 128:
@@ -245,7 +245,7 @@ def test_search_mfma2_ties_and_tombstones(rfx):
     q64 = osynth.to_f64(osynth.synth_rows(8, 0, 1, 768, "bf16"), "bf16")
     top = int(osearch.topk(q64, rows64, 1)[1][0, 0])
     kern, s, r = run_search_check(rindex, 20000, 768, "bf16", 256, 10, dup=(top, 3), tomb=[0, 7, 19999, top + 1])
-    assert kern == 5 and r[0, 0] == 3 and r[0, 1] == top
+    assert kern == 6 and r[0, 0] == 3 and r[0, 1] == top
 
 
 @pytest.mark.parametrize("nq", [65, 128, 129, 384, 512])
@@ -262,7 +262,7 @@ def test_search_mfma4_ragged_rows(rfx, n, dtype):
     """256-query-stationary kernel: 32-row tiles, ragged tails (NaN padding), fewer tiles than CUs."""
     rindex, _ = rfx
     kern, _, _ = run_search_check(rindex, n, 768, dtype, 256, 10)
-    assert kern == 5
+    assert kern == 6
 
 
 @pytest.mark.parametrize("nq,k", [(129, 10), (255, 1), (256, 4), (257, 10), (512, 5), (600, 10)])
@@ -270,7 +270,7 @@ def test_search_mfma4_query_groups(rfx, nq, k):
     """1..3 query groups of 256 (grid.y), padded last group, lane lists of 4 and 10."""
     rindex, _ = rfx
     kern, _, _ = run_search_check(rindex, 60_000, 768, "bf16", nq, k)
-    assert kern == 5
+    assert kern == 6
 
 
 def test_search_mfma4_many_duplicates(rfx):
@@ -290,7 +290,7 @@ def test_search_mfma4_many_duplicates(rfx):
     ix2.add(allr)
     q = rindex.synth_rows(8, 0, 256, 768, "bf16")
     s, r = ix2.search(q, 10)
-    assert ix2.plan(256, 10)[0] == 5
+    assert ix2.plan(256, 10)[0] == 6
     want = sorted(dst + [top])[:10]
     assert r[0].cpu().tolist() == want
     assert float(s[0, 0]) == float(s[0, 9])

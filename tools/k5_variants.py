@@ -27,7 +27,7 @@ ap.add_argument("--rows", type=int, default=10_000_000)
 ap.add_argument("--nq", type=int, default=256)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--burst", type=int, default=10)
-ap.add_argument("--modes", default="3,1000,132072,263144,394216,1009,132081,263153,394225,1003")
+ap.add_argument("--modes", default="3,1000,132072,20000000,1009,20000009,20000001,1003")
 ap.add_argument("--warm-seconds", type=float, default=2.0)
 a = ap.parse_args()
 f = _lib.lib.rfx_dbg_scan_variant
@@ -61,7 +61,7 @@ from rfx.index import topk_merge  # noqa: E402
 
 ref = None
 check = {}
-for m in [3] + [m for m in modes if m in (1000, 132072)]:
+for m in [3] + [m for m in modes if m in (1000, 132072, 20000000)]:
     launch(m)
     s, r = topk_merge(cs, cr, 10, list_len=ix.list_len(a.nq, 10))
     if ref is None:
