@@ -59,8 +59,8 @@ KERNEL_CASES = [
     (768, "f16", 100, 16, 3),  # 128-query-stationary
     (1024, "f16", 200, 10, 3),
     (256, "bf16", 200, 10, 2),  # 256x256 tiles, other d
-    (768, "bf16", 256, 10, 5),  # the config-3 kernel
-    (768, "f16", 300, 4, 5),    # kernel 5, KL 4, two query groups
+    (768, "bf16", 256, 10, 6),  # the config-3 kernel
+    (768, "f16", 300, 4, 6),    # kernel 6, KL 4, two query groups
 ]
 
 
