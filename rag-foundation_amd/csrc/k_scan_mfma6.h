@@ -10,17 +10,18 @@
 //     LDS bytes per FLOP as 32x32x16, and the chip holds a higher clock on it (MI355X_MICROARCH.md
 //     'DVFS give-back' item 7); measured -2.4 % on kernel 5.  The epilogue's query-pair swap is one
 //     v_permlane16_swap per register pair.
-//   * LDS image [8-row group][16-B chunk][row]: chunk c of row r of a stage slot at byte
-//     (r >> 3) * 4096 + c * 128 + (r & 7) * 16.  A lane's fragment for (row block rb, k-step kk)
-//     sits at a fixed per-lane base + rb * 8192 + kk * 512, so every ds_read_b128 takes its address
-//     from one base register and an immediate offset (kernel 5's XOR swizzle cost one v_add and one
-//     held offset register per k-step, and the kernel spilled).  The 16-lane groups of each read hit
-//     16 distinct bank quads (conflict-free).
-//   * An LDS-DMA piece (1 KB) is 8 rows × 128 B — whole 128-B lines of the corpus — and lands as
-//     one contiguous KB of the image: piece i = rows 8 (i >> 2) .. +7, chunks 8 (i & 3) .. +7.
+//   * LDS image of a stage slot: 16 pieces of 1 KB, piece i = rows i and i + 16 (512 B each),
+//     placed at i * 1056 B (a 32-B skew per piece).  Row r, 16-B chunk c sits at
+//     (r & 15) * 1056 + (r >> 4) * 512 + c * 16, so a lane's fragment for (row block rb, k-step kk)
+//     is a fixed per-lane base + rb * 512 + kk * 64: every ds_read_b128 takes its address from one
+//     base register and an immediate offset (kernel 5's XOR swizzle cost one v_add and one held
+//     offset register per k-step, and the kernel spilled).  The skew puts the 16 rows each 16-lane
+//     group of a ds_read_b128 reads into 16 distinct bank quads (conflict-free).
+//   * An LDS-DMA piece reads two 512-B row segments, like kernel 5 (a variant with 8 rows × 128 B
+//     pieces measured slower with the stream running).
 // Everything else as kernel 5: workgroup = 8 waves × 32 resident queries (192 VGPRs of B
 // fragments); 32-row tiles, block b takes tiles b, b + B, ...; a stage = 32 rows × 256 dims
-// (16 KB) in a 6-slot ring, 5 stages in flight, one counted vmcnt + s_barrier per stage; per-lane
+// (16 KB of rows) in a 6-slot ring, 5 stages in flight, one counted vmcnt + s_barrier per stage; per-lane
 // sorted top-KL lists in LDS behind a pruning bound shared across workgroups through a per-query
 // slot table (k_mfma_common.h fold / tau_min).
 // Requires the index invariant of rfx_api.hip: rows [nrows, capacity) are NaN and capacity is a
@@ -39,18 +40,19 @@ constexpr int kTM = 32;                   // rows per tile
 constexpr int kQW = 32;                   // queries per wave
 constexpr int kQG = kWaves * kQW;         // 256 queries per workgroup
 constexpr int kSK = 256;                  // dims per stage
-constexpr int kSlot = kTM * kSK * 2;      // 16 KB
+constexpr int kPiece = 1056;              // 1 KB of rows + a 32-B skew
+constexpr int kSlot = 16 * kPiece;        // 16.5 KB: 32 rows × 256 dims
 constexpr int kRing = 6;                  // 5 stages (80 KB) in flight
 constexpr int kGPW = 2;                   // LDS-DMA pieces per wave per stage (16 KB / 1 KB / 8 waves)
 constexpr int kTauW = 16;                 // u32 per query in the threshold table (KL <= 10 used)
-constexpr int kTauOff = kRing * kSlot;    // 96 KB
+constexpr int kTauOff = kRing * kSlot;    // 99 KB
 constexpr int kTauBytes = kQG * kTauW * 4;  // 16 KB: 16 DMA pieces, 2 per wave
 constexpr int kTauGPW = kTauBytes / 1024 / kWaves;
 constexpr int kListOff = kTauOff + kTauBytes;
 template <int KL>
 constexpr int lds_bytes() { return kListOff + kWaves * KL * 64 * 8; }  // + lane lists [wave][KL][64] u64
 static_assert(lds_bytes<10>() <= 163840, "LDS budget");
-static_assert(kSlot / 1024 == kWaves * kGPW && kTauGPW == 2, "DMA pieces per wave");
+static_assert(kTM * kSK * 2 / 1024 == kWaves * kGPW && kTauGPW == 2, "DMA pieces per wave");
 
 // Threshold-table refreshes go out after the last stage of tiles 0, 1, 3, 7, 11, ... (the lists
 // start empty, so the first tiles take the slow insert path until the slot table's bound arrives;
@@ -117,13 +119,13 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
     for (int ks = 0; ks < NKS; ++ks) bq[2 * ks + qb] = *(const uint4*)(qa + 32 * ks);
   }
 
-  // ---- LDS-DMA pieces: piece i = w + 8 u (u = 0, 1) of a stage = rows 8 (i >> 2) + (lane & 7),
-  // chunks 8 (i & 3) + (lane >> 3): 8 rows × 128 B, one contiguous KB of the slot image
+  // ---- LDS-DMA pieces: piece i = w + 8 u (u = 0, 1) of a stage = rows i (lanes 0-31) and i + 16
+  // (lanes 32-63), chunk lane & 31: two 512-B row segments, landing at i * kPiece
   uint32_t laneoff[kGPW];  // byte offset of this lane's 16 B inside a [32 rows][D] tile (stage 0)
 #pragma unroll
   for (int u = 0; u < kGPW; ++u) {
     const int i = w + kWaves * u;
-    laneoff[u] = (uint32_t)((8 * (i >> 2) + (lane & 7)) * D + (8 * (i & 3) + (lane >> 3)) * 8) * 2u;
+    laneoff[u] = (uint32_t)((i + 16 * half) * D + (lane & 31) * 8) * 2u;
   }
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
   const int64_t tile_stride = (int64_t)nblk * kTM * D;  // elements between a block's tiles
@@ -136,7 +138,7 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
     const int si = gi - ti * NST;
     const uint16_t* tbase = X + (int64_t)range * kTM * D + ti * tile_stride + si * kSK;
     bdma(make_rsrc(tbase), laneoff[u],
-         __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)(slot * kSlot) + (uint32_t)((w + kWaves * u) * 1024)));
+         __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)(slot * kSlot) + (uint32_t)((w + kWaves * u) * kPiece)));
   };
   const v4i32 tau_rsrc = make_rsrc(tau);
   auto issue_tau = [&]() {
@@ -152,16 +154,17 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
   const uint32_t slot_voff = (uint32_t)(q * kTauW + lst % KL) * 4u;
   const uint8_t* const tq = lds + kTauOff + (w * kQW + (lane & 15) + 16 * ((lane >> 4) & 1)) * (kTauW * 4);
   int n_slow = 0;  // (fold's diagnostic counter; unused here)
-  // A fragment of row block rb, k-step kk of a slot: per-lane base + rb * 8192 + kk * 512
-  const uint8_t* const frag_base = lds + ((lane >> 3) & 1) * 4096 + (lane >> 4) * 128 + (lane & 7) * 16;
+  // A fragment of row block rb, k-step kk of a slot (16x16x32: row 16 rb + (lane & 15), chunk
+  // 4 kk + (lane >> 4)): per-lane base + rb * 512 + kk * 64
+  const uint8_t* const frag_base = lds + (lane & 15) * kPiece + (lane >> 4) * 16;
   struct Frag {
     uint4 a[2];
   };
   auto read_frag = [&](int slot, int kk) -> Frag {
-    const uint8_t* p = frag_base + slot * kSlot + kk * 512;
+    const uint8_t* p = frag_base + slot * kSlot + kk * 64;
     Frag f;
     f.a[0] = *(const uint4*)p;
-    f.a[1] = *(const uint4*)(p + 8192);
+    f.a[1] = *(const uint4*)(p + 512);
     return f;
   };
 
