@@ -8,7 +8,7 @@ export PYTHONDONTWRITEBYTECODE=1
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 60 rocprofv3 -L > "$O/counters.txt" 2>&1 || true
 grep -oE "SQ_[A-Z0-9_]+|GRBM_[A-Z_]+|TCP_[A-Z0-9_]+|TA_[A-Z0-9_]+" "$O/counters.txt" | sort -u > "$O/counter_names.txt"
-MODES="--modes 3,1009,1003,132072 --rounds 1 --burst 3 --warm-seconds 1"
+MODES="--modes ${PMODES:-132072,20000000,20000009,1009,1003} --rounds 1 --burst 3 --warm-seconds 1"
 i=0
 run() {
   i=$((i+1))
@@ -23,9 +23,10 @@ O = sys.argv[1]
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for p in glob.glob(f"{O}/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(p)):
-        if "scan_mfma5" not in r["Kernel_Name"]:
+        kn = r["Kernel_Name"]
+        if "scan_mfma5" not in kn and "scan_mfma6" not in kn:
             continue
-        mode = r["Kernel_Name"].split("scan_mfma5_kernel<")[1].split(">")[0].split(",")[-1].strip()
+        mode = ("k5:" if "scan_mfma5" in kn else "k6:") + kn.split("_kernel<")[1].split(">")[0].split(",")[-1].strip()
         agg[mode][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for m, d in agg.items():
     print(m, {k: round(sum(v) / len(v) / 1e6, 3) for k, v in sorted(d.items())})

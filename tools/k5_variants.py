@@ -26,7 +26,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=10_000_000)
 ap.add_argument("--nq", type=int, default=256)
 ap.add_argument("--rounds", type=int, default=4)
-ap.add_argument("--burst", type=int, default=10)
+ap.add_argument("--burst", type=int, default=30)
 ap.add_argument("--modes", default="3,1000,132072,20000000,1009,20000009,20000001,1003")
 ap.add_argument("--warm-seconds", type=float, default=2.0)
 a = ap.parse_args()
@@ -74,7 +74,7 @@ while time.time() < t_end:
     torch.cuda.synchronize()
 res = {m: [] for m in modes}
 for rnd in range(a.rounds + 1):
-    for m in modes:
+    for m in (modes if rnd % 2 == 0 else modes[::-1]):  # alternate the order: no variant always follows the same one
         launch(m)  # settle into this variant
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
