@@ -42,16 +42,19 @@ constexpr int kQG = kWaves * kQW;         // 256 queries per workgroup
 constexpr int kSK = 256;                  // dims per stage
 constexpr int kPiece = 1056;              // 1 KB of rows + a 32-B skew
 constexpr int kSlot = 16 * kPiece;        // 16.5 KB: 32 rows × 256 dims
-constexpr int kRing = 6;                  // 5 stages (80 KB) in flight
+constexpr int kRing = 6;                  // default ring: 6 slots, 5 stages (80 KB of rows) in flight
 constexpr int kGPW = 2;                   // LDS-DMA pieces per wave per stage (16 KB / 1 KB / 8 waves)
 constexpr int kTauW = 16;                 // u32 per query in the threshold table (KL <= 10 used)
-constexpr int kTauOff = kRing * kSlot;    // 99 KB
 constexpr int kTauBytes = kQG * kTauW * 4;  // 16 KB: 16 DMA pieces, 2 per wave
 constexpr int kTauGPW = kTauBytes / 1024 / kWaves;
-constexpr int kListOff = kTauOff + kTauBytes;
-template <int KL>
-constexpr int lds_bytes() { return kListOff + kWaves * KL * 64 * 8; }  // + lane lists [wave][KL][64] u64
-static_assert(lds_bytes<10>() <= 163840, "LDS budget");
+// LDS: RING slots | threshold image | lane lists [wave][KL][64] u64
+template <int RING>
+constexpr int tau_off() { return RING * kSlot; }
+template <int RING>
+constexpr int list_off() { return tau_off<RING>() + kTauBytes; }
+template <int KL, int RING>
+constexpr int lds_bytes() { return list_off<RING>() + kWaves * KL * 64 * 8; }
+static_assert(lds_bytes<10, 6>() <= 163840 && lds_bytes<4, 7>() <= 163840, "LDS budget");
 static_assert(kTM * kSK * 2 / 1024 == kWaves * kGPW && kTauGPW == 2, "DMA pieces per wave");
 
 // Threshold-table refreshes go out after the last stage of tiles 0, 1, 3, 7, 11, ... (the lists
@@ -72,7 +75,7 @@ __device__ __forceinline__ void mask_rowmap1(V& a, uint32_t bits) {
 // 1 = no top-k epilogue (MFMAs kept live), 8 = no corpus stream after the prologue.
 constexpr int kModeMask = 2097152;
 
-template <int DT, int KL, int D, int MODE = 0>
+template <int DT, int KL, int D, int MODE = 0, int RING = kRing>
 __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Qp,
                                                             int nq, int ntiles, uint32_t* __restrict__ tau,
                                                             float* __restrict__ cand_s, int* __restrict__ cand_r,
@@ -82,7 +85,9 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
   constexpr int KPS = kSK / 32;  // k-steps per stage (8)
   static_assert(D % kSK == 0, "D must be a multiple of 256");
   static_assert(KL <= 10, "threshold table holds 10 slots");
-  __shared__ __attribute__((aligned(1024))) uint8_t lds[lds_bytes<KL>()];
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[lds_bytes<KL, RING>()];
+  constexpr int kTauOff = tau_off<RING>();
+  constexpr int kListOff = list_off<RING>();
 
   const int tid = threadIdx.x;
   const int w = tid >> 6, lane = tid & 63;
@@ -175,8 +180,8 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
   constexpr int PF = 1;
   constexpr int NF = PF + 1;
   constexpr int KB = KPS - PF;
-  constexpr int AHEAD = kRing - 1;
-  constexpr int YNG = (kRing - 2) * kGPW;  // ops younger than the next stage (8)
+  constexpr int AHEAD = RING - 1;
+  constexpr int YNG = (RING - 2) * kGPW;  // ops younger than the next stage (8 with 6 slots)
   static_assert((NST * KPS) % NF == 0, "fragment rotation must realign every tile");
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // resident queries landed before the counted stream
@@ -197,24 +202,30 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
     if constexpr ((MODE & 1) == 0)  // refreshed threshold image (issued 2 tiles ago; any value is a valid bound)
       if (it >= 2 && tau_refresh_tile(it - 2)) thr = max(thr, tau_min<KL>(tq));
     // A threshold refresh (kTauGPW ops) issued after the barrier of stage g_r = last stage of a
-    // refresh tile it_r is younger than stage g+1's pieces iff g-4 <= g_r <= g-1: at every stage of
-    // tile it_r + 1 and at stage 0 of tile it_r + 2 (overlaps admit one: stricter, never looser).
-    const bool tau_young12 = it >= 1 && tau_refresh_tile(it - 1);
-    const bool tau_young0 = tau_young12 || (it >= 2 && tau_refresh_tile(it - 2));
+    // refresh tile it_r is younger than stage g+1's pieces iff g-RING+2 <= g_r <= g-1, i.e. iff
+    // it - young_depth(s) <= it_r <= it - 1 (6 slots: it-2.. at stage 0, it-1 at stages 1, 2).
+    // Two young refreshes count as one: the wait is then stricter, never looser.
+    auto young = [&](int s) {
+      const int dmax = (RING - 3 + NST - s) / NST;
+      bool y = false;
+#pragma unroll
+      for (int d = 1; d <= dmax; ++d) y = y || (it >= d && tau_refresh_tile(it - d));
+      return y;
+    };
 #pragma unroll
     for (int s = 0; s < NST; ++s) {
       const int g = gbase + s;
-      const int slot = g % kRing;
+      const int slot = g % RING;
 #pragma unroll
       for (int kk = 0; kk < KPS; ++kk) {
         if constexpr ((MODE & 8) == 0)
-          if (kk % (KPS / kGPW) == 0) issue_piece(g + kRing - 1, (g + kRing - 1) % kRing, kk / (KPS / kGPW));
+          if (kk % (KPS / kGPW) == 0) issue_piece(g + RING - 1, (g + RING - 1) % RING, kk / (KPS / kGPW));
         if (kk == KB) {
           // stage g+1 landed for this wave: ops younger than its pieces = stages g+2..g+5 (8)
           // [+ a threshold refresh (2)]; lgkmcnt(0) + barrier: every wave has received its last
           // fragment of slot g, which may be refilled from here on.
           if constexpr ((MODE & 8) == 0) {
-            if (s == 0 ? tau_young0 : tau_young12)
+            if (young(s))
               asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(YNG + kTauGPW) : "memory");
             else
               asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(YNG) : "memory");
@@ -227,7 +238,7 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
         }
         const int ks = s * KPS + kk;
         // prefetch k-step kk + 1 (crossing into stage g+1 after the barrier)
-        fr[(ks + PF) % NF] = kk + PF < KPS ? read_frag(slot, kk + PF) : read_frag((g + 1) % kRing, kk + PF - KPS);
+        fr[(ks + PF) % NF] = kk + PF < KPS ? read_frag(slot, kk + PF) : read_frag((g + 1) % RING, kk + PF - KPS);
         const Frag& cur = fr[ks % NF];
         __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // the prefetch reads go out first
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);

@@ -25,6 +25,7 @@ from rfx.index import DeviceIndex, synth_rows  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=10_000_000)
 ap.add_argument("--nq", type=int, default=256)
+ap.add_argument("--k", type=int, default=10)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--burst", type=int, default=30)
 ap.add_argument("--modes", default="3,1000,132072,20000000,1009,20000009,20000001,1003")
@@ -40,10 +41,10 @@ g.restype = ctypes.c_int
 ix = DeviceIndex(768, "bf16", 0, capacity=a.rows)
 ix.add_synthetic(0, a.rows)
 q = synth_rows(1, 0, a.nq, 768, "bf16")
-_, ncand = ix.plan(a.nq, 10)
+_, ncand = ix.plan(a.nq, a.k)
 cs = torch.empty((a.nq, ncand), dtype=torch.float32, device="cuda")
 cr = torch.empty((a.nq, ncand), dtype=torch.int32, device="cuda")
-ws = torch.empty(ix.workspace_bytes(a.nq, 10), dtype=torch.uint8, device="cuda")
+ws = torch.empty(ix.workspace_bytes(a.nq, a.k), dtype=torch.uint8, device="cuda")
 scratch = torch.zeros(4, dtype=torch.int32, device="cuda")
 st = _lib.stream_ptr()
 modes = [int(m) for m in a.modes.split(",")] + [9]
@@ -53,7 +54,7 @@ def launch(m):
     if m == 9:
         _lib.check(g(ix.handle, _lib.ptr(scratch), st))
     else:
-        _lib.check(f(ix.handle, _lib.ptr(q), a.nq, 10, m, _lib.ptr(cs), _lib.ptr(cr), _lib.ptr(ws), ws.numel(), st))
+        _lib.check(f(ix.handle, _lib.ptr(q), a.nq, a.k, m, _lib.ptr(cs), _lib.ptr(cr), _lib.ptr(ws), ws.numel(), st))
 
 
 # correctness of the production-shaped variants against the production plan (exact rows)
@@ -61,9 +62,9 @@ from rfx.index import topk_merge  # noqa: E402
 
 ref = None
 check = {}
-for m in [3] + [m for m in modes if m in (1000, 132072, 20000000)]:
+for m in [3] + [m for m in modes if m in (1000, 132072, 20000000, 20000070, 20000071)]:
     launch(m)
-    s, r = topk_merge(cs, cr, 10, list_len=ix.list_len(a.nq, 10))
+    s, r = topk_merge(cs, cr, a.k, list_len=ix.list_len(a.nq, a.k))
     if ref is None:
         ref = (s.clone(), r.clone())
     check[m] = bool(torch.equal(r, ref[1])) and float((s - ref[0]).abs().max()) <= 1e-6
