@@ -89,6 +89,6 @@ for rnd in range(a.rounds + 1):
 alg = a.rows * 768 * 2
 out = {m: {"ms_median": round(sorted(v)[len(v) // 2], 4), "ms_min": round(min(v), 4),
            "GBps": round(alg / (sorted(v)[len(v) // 2] * 1e-3) / 1e9, 1)} for m, v in res.items()}
-for m, ok in check.items():
+for m, ok in [(m, ok) for m, ok in check.items() if m in out]:
     out[m]["rows_equal_production"] = ok
 print(json.dumps(out))
