@@ -37,6 +37,10 @@ int launch_scan_mfma6_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
     RFX_K6_DBG(1)
     RFX_K6_DBG(8)
     RFX_K6_DBG(9)
+    RFX_K6_DBG(16)
+    RFX_K6_DBG(32)
+    RFX_K6_DBG(48)
+    RFX_K6_DBG(41)
     default:
       return -1;
   }

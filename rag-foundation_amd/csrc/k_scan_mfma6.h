@@ -72,7 +72,9 @@ __device__ __forceinline__ void mask_rowmap1(V& a, uint32_t bits) {
 }
 
 // MODE: 0 production; kModeMask = row-masked variant (metadata filter); debug-build ablations:
-// 1 = no top-k epilogue (MFMAs kept live), 8 = no corpus stream after the prologue.
+// 1 = no top-k epilogue (MFMAs kept live), 8 = no corpus stream after the prologue, 16 = corpus
+// DMA with the non-temporal hint, 32 = every other k-step reuses the previous A fragments (half
+// the LDS reads; wrong scores, timing/energy only).
 constexpr int kModeMask = 2097152;
 
 template <int DT, int KL, int D, int MODE = 0, int RING = kRing>
@@ -142,8 +144,11 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
     const int ti = gi / NST;
     const int si = gi - ti * NST;
     const uint16_t* tbase = X + (int64_t)range * kTM * D + ti * tile_stride + si * kSK;
-    bdma(make_rsrc(tbase), laneoff[u],
-         __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)(slot * kSlot) + (uint32_t)((w + kWaves * u) * kPiece)));
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)(slot * kSlot) + (uint32_t)((w + kWaves * u) * kPiece));
+    if constexpr ((MODE & 16) != 0)
+      bdma_nt(make_rsrc(tbase), laneoff[u], dst);
+    else
+      bdma(make_rsrc(tbase), laneoff[u], dst);
   };
   const v4i32 tau_rsrc = make_rsrc(tau);
   auto issue_tau = [&]() {
@@ -238,7 +243,14 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
         }
         const int ks = s * KPS + kk;
         // prefetch k-step kk + 1 (crossing into stage g+1 after the barrier)
-        fr[(ks + PF) % NF] = kk + PF < KPS ? read_frag(slot, kk + PF) : read_frag((g + 1) % RING, kk + PF - KPS);
+        if constexpr ((MODE & 32) != 0) {
+          if ((ks & 1) == 0)
+            fr[(ks + PF) % NF] = fr[ks % NF];
+          else
+            fr[(ks + PF) % NF] = kk + PF < KPS ? read_frag(slot, kk + PF) : read_frag((g + 1) % RING, kk + PF - KPS);
+        } else {
+          fr[(ks + PF) % NF] = kk + PF < KPS ? read_frag(slot, kk + PF) : read_frag((g + 1) % RING, kk + PF - KPS);
+        }
         const Frag& cur = fr[ks % NF];
         __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // the prefetch reads go out first
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);

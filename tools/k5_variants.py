@@ -30,6 +30,7 @@ ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--burst", type=int, default=30)
 ap.add_argument("--modes", default="3,1000,132072,20000000,1009,20000009,20000001,1003")
 ap.add_argument("--warm-seconds", type=float, default=2.0)
+ap.add_argument("--no-stream-ref", action="store_true")
 a = ap.parse_args()
 f = _lib.lib.rfx_dbg_scan_variant
 f.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -47,7 +48,7 @@ cr = torch.empty((a.nq, ncand), dtype=torch.int32, device="cuda")
 ws = torch.empty(ix.workspace_bytes(a.nq, a.k), dtype=torch.uint8, device="cuda")
 scratch = torch.zeros(4, dtype=torch.int32, device="cuda")
 st = _lib.stream_ptr()
-modes = [int(m) for m in a.modes.split(",")] + [9]
+modes = [int(m) for m in a.modes.split(",")] + ([] if a.no_stream_ref else [9])
 
 
 def launch(m):
