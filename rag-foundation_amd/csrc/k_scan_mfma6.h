@@ -10,15 +10,16 @@
 //     LDS bytes per FLOP as 32x32x16, and the chip holds a higher clock on it (MI355X_MICROARCH.md
 //     'DVFS give-back' item 7); measured -2.4 % on kernel 5.  The epilogue's query-pair swap is one
 //     v_permlane16_swap per register pair.
-//   * LDS image of a stage slot: 16 pieces of 1 KB, piece i = rows i and i + 16 (512 B each),
-//     placed at i * 1056 B (a 32-B skew per piece).  Row r, 16-B chunk c sits at
-//     (r & 15) * 1056 + (r >> 4) * 512 + c * 16, so a lane's fragment for (row block rb, k-step kk)
-//     is a fixed per-lane base + rb * 512 + kk * 64: every ds_read_b128 takes its address from one
-//     base register and an immediate offset (kernel 5's XOR swizzle cost one v_add and one held
-//     offset register per k-step, and the kernel spilled).  The skew puts the 16 rows each 16-lane
-//     group of a ds_read_b128 reads into 16 distinct bank quads (conflict-free).
-//   * An LDS-DMA piece reads two 512-B row segments, like kernel 5 (a variant with 8 rows × 128 B
-//     pieces measured slower with the stream running).
+//   * LDS image of a stage slot: 16 pieces of 1 KB, piece i = tile rows 2i and 2i + 1 (512 B of
+//     each, the same two-row DMA shape as kernel 5), placed at i * 1056 B (a 32-B skew per piece).
+//     MFMA row m of row block rb is tile row 2m + rb, so row block rb reads one row out of each of
+//     the 16 pieces: a lane's fragment for (rb, k-step kk) sits at a fixed per-lane base
+//     ((lane & 15) * 1056 + (lane >> 4) * 16) + rb * 512 + kk * 64 and every ds_read_b128 takes its
+//     address from one base register and an immediate offset (kernel 5's XOR swizzle cost one
+//     v_add and one held offset register per k-step, and the kernel spilled).  The skew puts the 16
+//     rows each 16-lane group of a ds_read_b128 reads into 16 distinct bank quads (conflict-free).
+//     Measured alternatives (debug MODE bits): pieces of rows (i, i + 16), and 8 rows × 128 B
+//     pieces, both slower with the stream running.
 // Everything else as kernel 5: workgroup = 8 waves × 32 resident queries (192 VGPRs of B
 // fragments); 32-row tiles, block b takes tiles b, b + B, ...; a stage = 32 rows × 256 dims
 // (16 KB of rows) in a 6-slot ring, 5 stages in flight, one counted vmcnt + s_barrier per stage; per-lane
@@ -62,17 +63,21 @@ static_assert(kTM * kSK * 2 / 1024 == kWaves * kGPW && kTauGPW == 2, "DMA pieces
 // then every 4 tiles: a staler bound sends more lanes into the insert path — kernel 5 ablations).
 __device__ __forceinline__ bool tau_refresh_tile(int it) { return it < 2 || (it & 3) == 3; }
 
-// Metadata filter: row bit of the lane's value r after the epilogue's pair swap (fold ROWMAP 1,
-// bits pre-shifted by 8 * half): (r & 7) + 16 * (r >> 3).
-template <class V>
-__device__ __forceinline__ void mask_rowmap1(V& a, uint32_t bits) {
+// Metadata filter: row bit of the lane's value r after the epilogue's pair swap (fold ROWMAP 1 / 2,
+// bits pre-shifted by the lane's row base).
+template <int ROWMAP, class V>
+__device__ __forceinline__ void mask_rows(V& a, uint32_t bits) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r)
-    if (!((bits >> ((r & 7) + 16 * (r >> 3))) & 1u)) a[r >> 2][r & 3] = __builtin_nanf("");
+  for (int r = 0; r < 16; ++r) {
+    const int b = ROWMAP == 1 ? (r & 7) + 16 * (r >> 3) : 8 * ((r >> 2) & 1) + 2 * (r & 3) + (r >> 3);
+    if (!((bits >> b) & 1u)) a[r >> 2][r & 3] = __builtin_nanf("");
+  }
 }
 
 // MODE: 0 production; kModeMask = row-masked variant (metadata filter); debug-build ablations:
-// 1 = no top-k epilogue (MFMAs kept live), 8 = no corpus stream after the prologue, 16 = corpus
+// 1 = no top-k epilogue (MFMAs kept live), 8 = no corpus stream after the prologue, 64 = DMA
+// pieces of rows (i, i + 16) instead of (2i, 2i + 1) (row m of MFMA row block rb = tile row
+// 16 rb + m instead of 2 m + rb), 16 = corpus
 // DMA with the non-temporal hint, 32 = every other k-step reuses the previous A fragments (half
 // the LDS reads; wrong scores, timing/energy only).
 constexpr int kModeMask = 2097152;
@@ -126,13 +131,14 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
     for (int ks = 0; ks < NKS; ++ks) bq[2 * ks + qb] = *(const uint4*)(qa + 32 * ks);
   }
 
-  // ---- LDS-DMA pieces: piece i = w + 8 u (u = 0, 1) of a stage = rows i (lanes 0-31) and i + 16
-  // (lanes 32-63), chunk lane & 31: two 512-B row segments, landing at i * kPiece
+  // ---- LDS-DMA pieces: piece i = w + 8 u (u = 0, 1) of a stage = tile rows 2i (lanes 0-31) and
+  // 2i + 1 (lanes 32-63), chunk lane & 31: two 512-B row segments, landing at i * kPiece
   uint32_t laneoff[kGPW];  // byte offset of this lane's 16 B inside a [32 rows][D] tile (stage 0)
 #pragma unroll
   for (int u = 0; u < kGPW; ++u) {
     const int i = w + kWaves * u;
-    laneoff[u] = (uint32_t)((i + 16 * half) * D + (lane & 31) * 8) * 2u;
+    const int row = (MODE & 64) != 0 ? i + 16 * half : 2 * i + half;
+    laneoff[u] = (uint32_t)(row * D + (lane & 31) * 8) * 2u;
   }
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
   const int64_t tile_stride = (int64_t)nblk * kTM * D;  // elements between a block's tiles
@@ -275,8 +281,10 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
         acc4[2 * rb + 1][i] = __uint_as_float(r[1]);
       }
     if constexpr ((MODE & 1) == 0) {
-      if constexpr ((MODE & kModeMask) != 0) mask_rowmap1(acc4, mask[tile] >> (8 * half));
-      fold<KL, 1>(Acc4View{acc4}, Ls, thr, tile * kTM + 8 * half, tau_rsrc, slot_voff, n_slow);
+      constexpr int RM = (MODE & 64) != 0 ? 1 : 2;
+      const int rbase = tile * kTM + (RM == 1 ? 8 : 16) * half;
+      if constexpr ((MODE & kModeMask) != 0) mask_rows<RM>(acc4, mask[tile] >> (rbase - tile * kTM));
+      fold<KL, RM>(Acc4View{acc4}, Ls, thr, rbase, tau_rsrc, slot_voff, n_slow);
     } else {
       if (acc4[0][0] == 12345.f && acc4[1][1] == 54321.f && acc4[2][2] == 1.f && acc4[3][3] == 2.f) Ls[0] = 1;
     }
