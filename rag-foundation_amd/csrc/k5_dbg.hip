@@ -52,6 +52,7 @@ int launch_scan_mfma5_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
     RFX_K5_DBG(393225)
     RFX_K5_DBG(524288)
     RFX_K5_DBG(1048576)
+    RFX_K5_DBG(1179648)
     RFX_K5_DBG(257)
     RFX_K5_DBG(4194304)
     RFX_K5_DBG(4194320)

@@ -77,9 +77,8 @@ __device__ __forceinline__ void mask_rows(V& a, uint32_t bits) {
 // MODE: 0 production; kModeMask = row-masked variant (metadata filter); debug-build ablations:
 // 1 = no top-k epilogue (MFMAs kept live), 8 = no corpus stream after the prologue, 64 = DMA
 // pieces of rows (i, i + 16) instead of (2i, 2i + 1) (row m of MFMA row block rb = tile row
-// 16 rb + m instead of 2 m + rb), 16 = corpus
-// DMA with the non-temporal hint, 32 = every other k-step reuses the previous A fragments (half
-// the LDS reads; wrong scores, timing/energy only).
+// 16 rb + m instead of 2 m + rb), 16 = corpus DMA WITHOUT the non-temporal hint, 32 = every other
+// k-step reuses the previous A fragments (half the LDS reads; wrong scores, timing/energy only).
 constexpr int kModeMask = 2097152;
 
 template <int DT, int KL, int D, int MODE = 0, int RING = kRing>
@@ -151,10 +150,12 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
     const int si = gi - ti * NST;
     const uint16_t* tbase = X + (int64_t)range * kTM * D + ti * tile_stride + si * kSK;
     const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)(slot * kSlot) + (uint32_t)((w + kWaves * u) * kPiece));
+    // the corpus is read once per batch: non-temporal (measured at the power cap, 8-s bursts:
+    // -1.2 % against the default policy; the chip's time per batch is set by energy there)
     if constexpr ((MODE & 16) != 0)
-      bdma_nt(make_rsrc(tbase), laneoff[u], dst);
-    else
       bdma(make_rsrc(tbase), laneoff[u], dst);
+    else
+      bdma_nt(make_rsrc(tbase), laneoff[u], dst);
   };
   const v4i32 tau_rsrc = make_rsrc(tau);
   auto issue_tau = [&]() {
