@@ -10,16 +10,14 @@
 //     LDS bytes per FLOP as 32x32x16, and the chip holds a higher clock on it (MI355X_MICROARCH.md
 //     'DVFS give-back' item 7); measured -2.4 % on kernel 5.  The epilogue's query-pair swap is one
 //     v_permlane16_swap per register pair.
-//   * LDS image of a stage slot: 16 pieces of 1 KB, piece i = tile rows 2i and 2i + 1 (512 B of
-//     each, the same two-row DMA shape as kernel 5), placed at i * 1056 B (a 32-B skew per piece).
-//     MFMA row m of row block rb is tile row 2m + rb, so row block rb reads one row out of each of
-//     the 16 pieces: a lane's fragment for (rb, k-step kk) sits at a fixed per-lane base
-//     ((lane & 15) * 1056 + (lane >> 4) * 16) + rb * 512 + kk * 64 and every ds_read_b128 takes its
-//     address from one base register and an immediate offset (kernel 5's XOR swizzle cost one
-//     v_add and one held offset register per k-step, and the kernel spilled).  The skew puts the 16
-//     rows each 16-lane group of a ds_read_b128 reads into 16 distinct bank quads (conflict-free).
-//     Measured alternatives (debug MODE bits): pieces of rows (i, i + 16), and 8 rows × 128 B
-//     pieces, both slower with the stream running.
+//   * Non-temporal corpus DMA (the corpus is read once per batch).
+//   * No ablation code in the production template (kernel 5's MODE bits live in the debug build).
+// Why not more: the launch runs at the board's power cap (rocm-smi: 1400 W package power, sclk
+// 1.8-1.95 GHz, profiles/r02_power_*), so its time is the batch's energy over the cap; measured
+// alternatives that traded cycles for energy (tools/k5_variants.py, steady-state 8-s bursts):
+// an LDS image read with immediate offsets only (32-B skewed 1 KB pieces: no address VALU, no
+// spills, 13 % faster without the stream) took 2 % MORE time with the stream running (more stall
+// cycles at a higher clock), with 2-row or 8-row × 128 B pieces alike.
 // Everything else as kernel 5: workgroup = 8 waves × 32 resident queries (192 VGPRs of B
 // fragments); 32-row tiles, block b takes tiles b, b + B, ...; a stage = 32 rows × 256 dims
 // (16 KB of rows) in a 6-slot ring, 5 stages in flight, one counted vmcnt + s_barrier per stage; per-lane
@@ -41,9 +39,9 @@ constexpr int kTM = 32;                   // rows per tile
 constexpr int kQW = 32;                   // queries per wave
 constexpr int kQG = kWaves * kQW;         // 256 queries per workgroup
 constexpr int kSK = 256;                  // dims per stage
-constexpr int kPiece = 1056;              // 1 KB of rows + a 32-B skew
-constexpr int kSlot = 16 * kPiece;        // 16.5 KB: 32 rows × 256 dims
-constexpr int kRing = 6;                  // default ring: 6 slots, 5 stages (80 KB of rows) in flight
+constexpr int kRowB = kSK * 2;            // 512 B per row per stage
+constexpr int kSlot = kTM * kRowB;        // 16 KB: 32 rows × 256 dims
+constexpr int kRing = 6;                  // default ring: 6 slots, 5 stages (80 KB) in flight
 constexpr int kGPW = 2;                   // LDS-DMA pieces per wave per stage (16 KB / 1 KB / 8 waves)
 constexpr int kTauW = 16;                 // u32 per query in the threshold table (KL <= 10 used)
 constexpr int kTauBytes = kQG * kTauW * 4;  // 16 KB: 16 DMA pieces, 2 per wave
@@ -56,29 +54,26 @@ constexpr int list_off() { return tau_off<RING>() + kTauBytes; }
 template <int KL, int RING>
 constexpr int lds_bytes() { return list_off<RING>() + kWaves * KL * 64 * 8; }
 static_assert(lds_bytes<10, 6>() <= 163840 && lds_bytes<4, 7>() <= 163840, "LDS budget");
-static_assert(kTM * kSK * 2 / 1024 == kWaves * kGPW && kTauGPW == 2, "DMA pieces per wave");
+static_assert(kSlot / 1024 == kWaves * kGPW && kTauGPW == 2, "DMA pieces per wave");
 
 // Threshold-table refreshes go out after the last stage of tiles 0, 1, 3, 7, 11, ... (the lists
 // start empty, so the first tiles take the slow insert path until the slot table's bound arrives;
 // then every 4 tiles: a staler bound sends more lanes into the insert path — kernel 5 ablations).
 __device__ __forceinline__ bool tau_refresh_tile(int it) { return it < 2 || (it & 3) == 3; }
 
-// Metadata filter: row bit of the lane's value r after the epilogue's pair swap (fold ROWMAP 1 / 2,
-// bits pre-shifted by the lane's row base).
-template <int ROWMAP, class V>
-__device__ __forceinline__ void mask_rows(V& a, uint32_t bits) {
+// Metadata filter: row bit of the lane's value r after the epilogue's pair swap (fold ROWMAP 1,
+// bits pre-shifted by 8 * half): (r & 7) + 16 * (r >> 3).
+template <class V>
+__device__ __forceinline__ void mask_rowmap1(V& a, uint32_t bits) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int b = ROWMAP == 1 ? (r & 7) + 16 * (r >> 3) : 8 * ((r >> 2) & 1) + 2 * (r & 3) + (r >> 3);
-    if (!((bits >> b) & 1u)) a[r >> 2][r & 3] = __builtin_nanf("");
-  }
+  for (int r = 0; r < 16; ++r)
+    if (!((bits >> ((r & 7) + 16 * (r >> 3))) & 1u)) a[r >> 2][r & 3] = __builtin_nanf("");
 }
 
 // MODE: 0 production; kModeMask = row-masked variant (metadata filter); debug-build ablations:
-// 1 = no top-k epilogue (MFMAs kept live), 8 = no corpus stream after the prologue, 64 = DMA
-// pieces of rows (i, i + 16) instead of (2i, 2i + 1) (row m of MFMA row block rb = tile row
-// 16 rb + m instead of 2 m + rb), 16 = corpus DMA WITHOUT the non-temporal hint, 32 = every other
-// k-step reuses the previous A fragments (half the LDS reads; wrong scores, timing/energy only).
+// 1 = no top-k epilogue (MFMAs kept live), 8 = no corpus stream after the prologue, 16 = corpus
+// DMA WITHOUT the non-temporal hint, 32 = every other k-step reuses the previous A fragments (half
+// the LDS reads; wrong scores, timing/energy only).
 constexpr int kModeMask = 2097152;
 
 template <int DT, int KL, int D, int MODE = 0, int RING = kRing>
@@ -130,14 +125,15 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
     for (int ks = 0; ks < NKS; ++ks) bq[2 * ks + qb] = *(const uint4*)(qa + 32 * ks);
   }
 
-  // ---- LDS-DMA pieces: piece i = w + 8 u (u = 0, 1) of a stage = tile rows 2i (lanes 0-31) and
-  // 2i + 1 (lanes 32-63), chunk lane & 31: two 512-B row segments, landing at i * kPiece
+  // ---- LDS-DMA pieces: piece i = w + 8 u (u = 0, 1) of a stage fills slot bytes [1024 i, +1024) =
+  // rows 2i, 2i+1 (512 B each); lane -> (row 2i + half, position lane & 31) <- source chunk
+  // position ^ (row & 15): the 16 rows a 16-lane group of a fragment read touches sit in 16
+  // distinct bank quads (the permutation rides on the DMA source address)
   uint32_t laneoff[kGPW];  // byte offset of this lane's 16 B inside a [32 rows][D] tile (stage 0)
 #pragma unroll
   for (int u = 0; u < kGPW; ++u) {
-    const int i = w + kWaves * u;
-    const int row = (MODE & 64) != 0 ? i + 16 * half : 2 * i + half;
-    laneoff[u] = (uint32_t)(row * D + (lane & 31) * 8) * 2u;
+    const int r = 2 * (w + kWaves * u) + half;
+    laneoff[u] = (uint32_t)(r * D + (((lane & 31) ^ (r & 15)) * 8)) * 2u;
   }
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
   const int64_t tile_stride = (int64_t)nblk * kTM * D;  // elements between a block's tiles
@@ -149,7 +145,7 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
     const int ti = gi / NST;
     const int si = gi - ti * NST;
     const uint16_t* tbase = X + (int64_t)range * kTM * D + ti * tile_stride + si * kSK;
-    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)(slot * kSlot) + (uint32_t)((w + kWaves * u) * kPiece));
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)(slot * kSlot) + (uint32_t)((w + kWaves * u) * 1024));
     // the corpus is read once per batch: non-temporal (measured at the power cap, 8-s bursts:
     // -1.2 % against the default policy; the chip's time per batch is set by energy there)
     if constexpr ((MODE & 16) != 0)
@@ -171,17 +167,18 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
   const uint32_t slot_voff = (uint32_t)(q * kTauW + lst % KL) * 4u;
   const uint8_t* const tq = lds + kTauOff + (w * kQW + (lane & 15) + 16 * ((lane >> 4) & 1)) * (kTauW * 4);
   int n_slow = 0;  // (fold's diagnostic counter; unused here)
-  // A fragment of row block rb, k-step kk of a slot (16x16x32: row 16 rb + (lane & 15), chunk
-  // 4 kk + (lane >> 4)): per-lane base + rb * 512 + kk * 64
-  const uint8_t* const frag_base = lds + (lane & 15) * kPiece + (lane >> 4) * 16;
+  // A fragment of row block rb, k-step kk of a slot (16x16x32): row 16 rb + (lane & 15), chunk
+  // 4 kk + (lane >> 4), stored at position chunk ^ (row & 15); the two row blocks are 8 KB apart
+  const uint8_t* const frag_base = lds + (lane & 15) * kRowB;
+  const int sw = lane & 15;
   struct Frag {
     uint4 a[2];
   };
   auto read_frag = [&](int slot, int kk) -> Frag {
-    const uint8_t* p = frag_base + slot * kSlot + kk * 64;
+    const uint8_t* p = frag_base + slot * kSlot + (((4 * kk + (lane >> 4)) ^ sw) << 4);
     Frag f;
     f.a[0] = *(const uint4*)p;
-    f.a[1] = *(const uint4*)(p + 512);
+    f.a[1] = *(const uint4*)(p + 16 * kRowB);
     return f;
   };
 
@@ -282,10 +279,8 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
         acc4[2 * rb + 1][i] = __uint_as_float(r[1]);
       }
     if constexpr ((MODE & 1) == 0) {
-      constexpr int RM = (MODE & 64) != 0 ? 1 : 2;
-      const int rbase = tile * kTM + (RM == 1 ? 8 : 16) * half;
-      if constexpr ((MODE & kModeMask) != 0) mask_rows<RM>(acc4, mask[tile] >> (rbase - tile * kTM));
-      fold<KL, RM>(Acc4View{acc4}, Ls, thr, rbase, tau_rsrc, slot_voff, n_slow);
+      if constexpr ((MODE & kModeMask) != 0) mask_rowmap1(acc4, mask[tile] >> (8 * half));
+      fold<KL, 1>(Acc4View{acc4}, Ls, thr, tile * kTM + 8 * half, tau_rsrc, slot_voff, n_slow);
     } else {
       if (acc4[0][0] == 12345.f && acc4[1][1] == 54321.f && acc4[2][2] == 1.f && acc4[3][3] == 2.f) Ls[0] = 1;
     }
