@@ -164,8 +164,8 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
   if (L.kernel) {
     L.n_cand = L.mp.n_lists * L.mp.k_lane;
     L.q_bytes = (size_t)L.mp.nq_pad * ix.dim * 2;
-    if (L.kernel == 6)  // (>= kernel 5's table: the debug build runs either on this layout)
-      tau_bytes = std::max(rfx::tau_bytes_mfma6(L.mp), rfx::tau_bytes_mfma5(L.mp));
+    if (L.kernel == 6)  // (the debug build's kernel-5 ablations use the same [nq_pad][16] table)
+      tau_bytes = rfx::tau_bytes_mfma6(L.mp);
     else if (L.kernel >= 2)
       tau_bytes = (size_t)(L.mp.nq_pad + 256) * 4;  // + slack: 1 KB threshold DMA per group
   } else {
@@ -249,7 +249,6 @@ int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq,
     uint32_t* tau = (uint32_t*)(ws + L.tau_off);
     const int rc =
         L.kernel == 6 ? rfx::launch_scan_mfma6(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
-        : L.kernel == 5 ? rfx::launch_scan_mfma5(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
         : L.kernel == 3 ? rfx::launch_scan_mfma3(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
         : L.kernel == 2 ? rfx::launch_scan_mfma2(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
                         : rfx::launch_scan_mfma(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, cs, cr, st, mask);
