@@ -70,3 +70,16 @@ def finish_frame_payload(*, prompt_tokens, completion_tokens, model):
     return {"type": "finish", "finishReason": "stop", "promptTokens": prompt_tokens,
             "completionTokens": completion_tokens,
             "usage": {"prompt_tokens": prompt_tokens, "completion_tokens": completion_tokens, "model": model}}
+
+
+def harness_citations(frames):
+    """The benchmark harness's reading of a chat stream (scripts/benchmark/run_benchmark.py:
+    196-216): every "source-document" frame becomes {title, snippet, sourceId}."""
+    out = []
+    for f in frames:
+        if not f.startswith("data:") or f.strip() == "data: [DONE]":
+            continue
+        p = json.loads(f.split(": ", 1)[1])
+        if p.get("type") == "source-document":
+            out.append({"title": p.get("title"), "snippet": p.get("snippet"), "sourceId": p.get("sourceId")})
+    return out

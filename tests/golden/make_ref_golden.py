@@ -6,6 +6,8 @@ does not exist on the GPU box).  Output files are committed data fixtures:
                        from /root/reference; nothing is stubbed)
   sample_report.md     docs/demo/sample-report.md (BASELINE config 1 input document, data)
   bench_questions.json scripts/benchmark/datasets/sample/questions.jsonl questions (data)
+  ref_citation_hit.json inputs -> reference scripts/benchmark/metrics.py:citation_hit outputs
+                       (citation dicts shaped as run_benchmark.py:209-216 parses them)
 
 Usage: python tests/golden/make_ref_golden.py [/root/reference]
 """
@@ -46,7 +48,20 @@ def main():
         f.write(sample)
     with open(os.path.join(HERE, "bench_questions.json"), "w") as f:
         json.dump({"source": "scripts/benchmark/datasets/sample/questions.jsonl", "questions": qs}, f, indent=1)
-    print(f"wrote {len(out)} normalize cases, sample report ({len(sample)} B), {len(qs)} questions")
+    hit_cases = [
+        ([], ["a.md"]), ([{"title": "a.md"}], []), ([{"title": "A.MD"}], ["a.md"]),
+        ([{"title": "b.md", "sourceId": "cit-0"}], ["b.md"]), ([{"title": "b.md", "sourceId": "cit-0"}], ["cit-0"]),
+        ([{"sourceId": "cit-1", "title": "x"}, {"title": "y"}], ["y"]), ([{"uri": "local://s/f#chunk-3"}], ["local://s/f#chunk-3"]),
+        ([{"doc_id": "D1", "title": "t"}], ["d1"]), ([{"title": None, "snippet": "s"}], ["s"]),
+        ([{"title": "sample-report.md", "snippet": "x", "sourceId": "cit-0"}, {"title": "other.md", "sourceId": "cit-1"}],
+         ["sample-report.md", "other.md"]),
+    ]
+    hits = [{"citations": c, "gold": g, "citation_hit": mod.citation_hit(c, g)} for c, g in hit_cases]
+    with open(os.path.join(HERE, "ref_citation_hit.json"), "w") as f:
+        json.dump({"source": "scripts/benchmark/metrics.py:73-92 (citation_hit), imported from the reference",
+                   "cases": hits}, f, indent=1)
+    print(f"wrote {len(out)} normalize cases, sample report ({len(sample)} B), {len(qs)} questions, "
+          f"{len(hits)} citation_hit cases")
 
 
 if __name__ == "__main__":

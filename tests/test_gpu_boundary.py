@@ -41,3 +41,35 @@ def test_cfg1_frames_k1_k5(golden_dir, tmp_path, dtype):
                              ["sample-report.md"] * k, [g.retrieved_context.text for g in gc])
             assert all(c["store"] == st for c in cits)
     rag.delete_store(st)
+
+
+def test_multi_store_union_on_gpu(golden_dir, tmp_path):
+    """ask_stream over several stores (gemini_rag.py:463-469 store_names list): the hits are the
+    union's top-k in (score desc, store order, row asc); every hit's score is within 1e-5 of the
+    oracle's f64 score of that chunk (oracle embedder, bit-exact with the GPU one)."""
+    import numpy as np
+
+    from fakes import OracleRetriever
+    from rfx import store as rstore
+    from rfx.retriever import GpuRetriever
+
+    rstore.set_registry(rstore.StoreRegistry(root=str(tmp_path), device=0))
+    ret = GpuRetriever(dtype="f32")
+    orc = OracleRetriever()
+    text = open(os.path.join(golden_dir, "sample_report.md"), encoding="utf-8").read()
+    docs = [text, "mock mode document assistant citations retrieval " * 12, text.upper(), "unrelated words " * 30]
+    names = [ret.create_store(f"s{i}") for i in range(3)]
+    for i, d in enumerate(docs):
+        ret.add_document(names[i % 3], d, f"d{i}", {"white_space_config": {"max_tokens_per_chunk": 4,
+                                                                            "max_overlap_tokens": 1}})
+    for q in ["document assistant citations", "sample report", "unrelated"]:
+        for k in (1, 5, 12):
+            hits = ret.search(names, q, k)
+            singles = [(h.score, si, h.row) for si, n in enumerate(names) for h in ret.search([n], q, k)]
+            want = sorted(singles, key=lambda t: (-t[0], t[1], t[2]))[:k]
+            assert [(h.score, names.index(h.store), h.row) for h in hits] == want
+            qv = orc._embed([q])[0]
+            for h in hits:
+                ref = float(orc._embed([h.text])[0] @ qv)
+                assert abs(h.score - ref) <= 1e-5, (h.text, h.score, ref)
+            assert np.all(np.diff([h.score for h in hits]) <= 0)
