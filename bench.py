@@ -81,13 +81,20 @@ def cpu_model():
     return platform.processor()
 
 
-def load_pmc_traffic(workload_key):
-    """HBM bytes per scan launch from the committed rocprofv3 PMC summary (profiles/), or None."""
+KERNEL_NAMES = {0: "scan_valu_kernel", 1: "scan_mfma_kernel", 2: "scan_mfma2_kernel", 3: "scan_mfma3_kernel",
+                4: "scan_mfma4_kernel", 5: "scan_mfma5_kernel", 6: "scan_mfma6_kernel"}
+
+
+def load_pmc_traffic(workload_key, kernel_name):
+    """HBM bytes per scan launch from the committed rocprofv3 PMC summary (profiles/), or None —
+    also None when that summary was taken on another kernel than the one this run launched."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(p))
         e = d.get(workload_key)
-        return None if e is None else float(e["hbm_bytes_per_launch"])
+        if e is None or e.get("kernel_match") not in kernel_name:
+            return None
+        return float(e["hbm_bytes_per_launch"])
     except (OSError, ValueError, KeyError, TypeError):
         return None
 
@@ -126,6 +133,7 @@ def main():
     ix = ixs[0]
     q = synth_rows(a.seed + 1, 0, a.nq, a.dim, a.dtype, local)
     kern, n_cand = ix.plan(a.nq, a.k)
+    kname = KERNEL_NAMES[kern]
     list_len = ix.list_len(a.nq, a.k)  # sorted candidate lists: the merge bounds by their k-th entries
     rec = torch.empty((a.nq, a.k, 2), dtype=torch.int64, device=dev)
     ws = torch.empty(max(ix.workspace_bytes(a.nq, a.k), 1), dtype=torch.uint8, device=dev)
@@ -212,9 +220,8 @@ def main():
         "achieved_hbm_gbps_per_gpu": round(achieved, 1),
         "build_id": _lib.BUILD_ID,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": load_pmc_traffic(workload_key),
-                     "kernel": {0: "scan_valu_kernel", 1: "scan_mfma_kernel", 2: "scan_mfma2_kernel", 3: "scan_mfma3_kernel",
-                                4: "scan_mfma4_kernel", 5: "scan_mfma5_kernel", 6: "scan_mfma6_kernel"}[kern],
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": load_pmc_traffic(workload_key, kname),
+                     "kernel": kname,
                      "kernel_ms": round(scan_ms, 4), "alg_bytes_per_launch": alg_bytes},
     }
 

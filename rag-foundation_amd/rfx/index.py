@@ -51,6 +51,14 @@ class DeviceIndex:
         with torch.cuda.device(self.device):
             check(lib.rfx_rows_sync(self.handle, path.encode(), int(upto), int(file_base)))
 
+    def data_ptr(self) -> int:
+        """Device address of row 0 (rows contiguous, row-major, tombstoned rows NaN).  Valid until
+        the next add / reserve / rows_sync, which may reallocate: the owner's lock must be held
+        across every use (rfx.store.LocalStore.search)."""
+        p = ctypes.c_void_p()
+        check(lib.rfx_index_data(self.handle, ctypes.byref(p)))
+        return p.value
+
     def mask_tensor(self, words):
         """Row-mask words (numpy int32) as the device tensor the masked search takes."""
         return torch.from_numpy(words).to(self._dev())

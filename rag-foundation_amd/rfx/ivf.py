@@ -157,6 +157,9 @@ class IvfIndex:
         rdt = {v: k_ for k_, v in _lib.TORCH_DTYPES.items()}.get(rows.dtype)
         if rdt is None:
             raise ValueError("rows must be float32, bfloat16 or float16")
+        return self._rerank(q, dt, k, nprobe, ptr(rows), _lib.DTYPE_CODES[rdt], rerank_k, stream)
+
+    def _rerank(self, q, dt, k, nprobe, rows_p, rows_code, rerank_k, stream):
         rk = max(int(k), 16) if rerank_k is None else int(rerank_k)
         nq = q.shape[0]
         out_s = torch.empty((nq, k), dtype=torch.float32, device=self._dev())
@@ -165,10 +168,49 @@ class IvfIndex:
         check(lib.rfx_ivf_rerank_workspace_bytes(self.handle, nq, int(k), int(nprobe), rk, ctypes.byref(b)))
         ws = torch.empty(max(b.value, 1), dtype=torch.uint8, device=self._dev())
         with torch.cuda.device(self.device):
-            check(lib.rfx_ivf_search_rerank(self.handle, ptr(q), nq, dt, int(k), int(nprobe), rk, ptr(rows),
-                                            _lib.DTYPE_CODES[rdt], ptr(out_s), ptr(out_r), ptr(ws), ws.numel(),
-                                            stream_ptr(stream)))
+            check(lib.rfx_ivf_search_rerank(self.handle, ptr(q), nq, dt, int(k), int(nprobe), rk, rows_p, rows_code,
+                                            ptr(out_s), ptr(out_r), ptr(ws), ws.numel(), stream_ptr(stream)))
         return out_s, out_r
+
+    # ---- serving from a store's DeviceIndex (rfx.store, config 5) ------------------------------------
+    def search_index(self, queries: torch.Tensor, k: int, nprobe: int, index, rerank_k: int = None, stream=None):
+        """search_rerank against a DeviceIndex holding the same rows in the same order (row i of
+        this index = row i of `index`).  Tombstoned rows are NaN there, so the exact re-rank drops
+        them.  The caller holds the index owner's lock until the results are read (data_ptr)."""
+        q, dt = self._rows(queries)
+        if index.dim != self.dim or index.device != self.device:
+            raise ValueError("index dim / device differ from the IVF index")
+        if index.rows < self.rows:
+            raise ValueError(f"index holds {index.rows} rows, the IVF lists {self.rows}")
+        return self._rerank(q, dt, k, nprobe, ctypes.c_void_p(index.data_ptr()), _lib.DTYPE_CODES[index.dtype],
+                            rerank_k, stream)
+
+    def train_from(self, index, row_ids, iters: int = 10) -> None:
+        """k-means over the rows `row_ids` (sorted int64 numpy array) of a DeviceIndex."""
+        import numpy as np
+        ids = np.asarray(row_ids, dtype=np.int64)
+        parts, span = [], 1 << 20
+        for r0 in range(0, int(ids[-1]) + 1 if ids.size else 0, span):
+            sel = ids[(ids >= r0) & (ids < r0 + span)] - r0
+            if sel.size:
+                m = int(sel[-1]) + 1
+                parts.append(index.read(r0, m)[torch.from_numpy(sel).to(self._dev())])
+        self.train(torch.cat(parts) if parts else torch.empty((0, self.dim), device=self._dev()), iters)
+
+    def add_from(self, index, upto: int) -> None:
+        """Assign rows [self.rows, upto) of a DeviceIndex to their lists (1M-row pieces)."""
+        span = 1 << 20
+        while self.rows < upto:
+            r0 = self.rows
+            self.add(index.read(r0, min(span, upto - r0)))
+
+    def centroid_bytes(self) -> bytes:
+        return self.centroids()[0].cpu().numpy().tobytes()
+
+    def load_centroids(self, raw: bytes) -> None:
+        import numpy as np
+        qc = np.frombuffer(raw, dtype=np.int8).reshape(self.nlist, self.dim)
+        self.set_centroids(torch.from_numpy(qc.copy()).to(self._dev()))
 
 
 def quantize(rows: torch.Tensor, stream=None):

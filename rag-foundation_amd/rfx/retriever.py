@@ -108,7 +108,7 @@ class GpuRetriever:
         kmax = max(k for _, k in items)
         with torch.cuda.device(st.device):
             q = self.embedder(st.dim).embed_texts([t for t, _ in items], st.dtype)
-            s, r = st.index.search(q, kmax, row_mask=row_mask)
+            s, r = st.search(q, kmax, row_mask=row_mask)
             s, r = s.cpu().tolist(), r.cpu().tolist()
         return [(s[i][:k], r[i][:k]) for i, (_, k) in enumerate(items)]
 

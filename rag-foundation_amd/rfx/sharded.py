@@ -32,6 +32,8 @@ def parse_devices(spec: str):
 
 
 class ShardedIndex:
+    supports_ivf = False  # IVF stores keep the exact scan when row-sharded (rfx.store)
+
     def __init__(self, dim, dtype, devices):
         if not devices:
             raise ValueError("need at least one device")

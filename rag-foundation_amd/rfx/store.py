@@ -8,16 +8,27 @@ On-disk layout of a store (directory <root>/<store id>/), every data file APPEND
   files.jsonl   file records: {"op": "add", "id", "first", "n", "display_name", "uri", "metadata"}
                 and {"op": "del", "id"}
   tombs.bin     int64 row ids of deleted rows
+  ivf-<id>.bin  (IVF stores) k-means centroids: "RFXCENT1", u32 nlist, u32 dim, 4 zero bytes,
+                then int8 [nlist][dim]; written once per training, never modified
   manifest.json the commit point: {"format": 2, "name", "display_name", "dim", "dtype",
-                "generation", "version", "rows", "meta_bytes", "files_bytes", "tombs"} — the
-                committed length of every file above; replaced atomically (rename) after the
-                appended bytes are fsync'ed.  Readers never read past it, so a writer that dies
-                mid-append leaves a tail that is ignored, and cut by the next writer.
+                "generation", "version", "rows", "meta_bytes", "files_bytes", "tombs",
+                "index": {"kind": "flat"|"ivf", "nlist", "nprobe", "train_min"},
+                "ivf": null | {"id", "rows"}} — the committed length of every file above;
+                replaced atomically (rename) after the appended bytes are fsync'ed.  Readers
+                never read past it, so a writer that dies mid-append leaves a tail that is
+                ignored, and cut by the next writer.
   .lock         fcntl writer lock: appends from several processes (ARQ worker max_jobs=10,
                 worker.py:125; several workers) serialise on it, each first catching up with
                 what the others committed.
 An upload costs O(its own rows) of disk and device work; a reader (API process) that sees a
 newer manifest loads only what was appended since its last look (rows, metadata, tombstones).
+
+IVF stores (RFX_INDEX=ivf at creation): the writer trains k-means on the
+live rows once there are train_min of them (again at every 8x growth) and commits the centroids
+file with the manifest; every process keeps an IvfIndex (rfx.ivf) over the same rows in the same
+order, built from the committed centroids and extended incrementally as rows arrive.  Unfiltered
+searches probe nprobe lists and re-rank the candidates exactly against the DeviceIndex rows (so
+tombstones, NaN there, never return); filtered searches and untrained stores use the exact scan.
 
 GPU state is a process-level singleton (StoreRegistry), because get_rag_client() builds a new
 adapter per request (chat.py:937, ingestion.py:214).
@@ -39,6 +50,21 @@ from .index import DeviceIndex
 
 STORE_PREFIX = "fileSearchStores/"  # accepted by routes/stores.py:46 (prefix check)
 FORMAT = 2
+_CENT_MAGIC = b"RFXCENT1"
+
+
+def index_spec_from_env():
+    """Index kind of new stores: RFX_INDEX=flat (default, exact scan) | ivf (RFX_IVF_NLIST lists,
+    default 1024; RFX_IVF_NPROBE, default 32; trained at RFX_IVF_TRAIN_MIN live rows, default
+    32 x nlist)."""
+    kind = os.environ.get("RFX_INDEX", "flat")
+    if kind == "flat":
+        return {"kind": "flat"}
+    if kind != "ivf":
+        raise ValueError(f"RFX_INDEX={kind!r}: expected flat or ivf")
+    nlist = int(os.environ.get("RFX_IVF_NLIST", "1024"))
+    return {"kind": "ivf", "nlist": nlist, "nprobe": min(int(os.environ.get("RFX_IVF_NPROBE", "32")), nlist, 64),
+            "train_min": int(os.environ.get("RFX_IVF_TRAIN_MIN", str(32 * nlist)))}
 
 
 def default_root() -> str:
@@ -89,11 +115,14 @@ class LocalStore:
     # the vector store behind a LocalStore: DeviceIndex (HIP) in the product; tests inject a host
     # stand-in with the same interface to exercise the file protocol without a GPU
     index_factory = DeviceIndex
+    ivf_factory = None  # rfx.ivf.IvfIndex (imported on first use); tests inject a host stand-in
 
-    def __init__(self, path, device, index_factory=None):
+    def __init__(self, path, device, index_factory=None, ivf_factory=None):
         self.path, self.device = path, int(device)
         if index_factory is not None:
             self.index_factory = index_factory
+        if ivf_factory is not None:
+            self.ivf_factory = ivf_factory
         self.name = self.display_name = None
         self.dim = self.dtype = None
         self.generation = None
@@ -105,6 +134,10 @@ class LocalStore:
         self.lock = threading.RLock()
         self._stat = None
         self._masks = {}    # (version, filter key) -> device row mask
+        self.spec = {"kind": "flat"}
+        self.ivf_meta = None  # committed {"id", "rows"} of the current centroids
+        self.ivf = None       # this process's IvfIndex over the committed rows
+        self.ivf_id = None
 
     # ---- files -------------------------------------------------------------------------------
     def _p(self, name):
@@ -125,7 +158,7 @@ class LocalStore:
         man = {"format": FORMAT, "name": self.name, "display_name": self.display_name, "dim": self.dim,
                "dtype": self.dtype, "generation": self.generation, "version": self.version,
                "rows": len(self.rows), "meta_bytes": self.meta_bytes, "files_bytes": self.files_bytes,
-               "tombs": self.tombs}
+               "tombs": self.tombs, "index": self.spec, "ivf": self.ivf_meta}
         tmp = self._p(f"manifest.json.{os.getpid()}.{threading.get_ident()}.tmp")
         with open(tmp, "w", encoding="utf-8") as f:
             json.dump(man, f)
@@ -167,10 +200,12 @@ class LocalStore:
 
     # ---- create / open / catch up ---------------------------------------------------------------
     @classmethod
-    def create(cls, path, name, display_name, dim, dtype, device, index_factory=None):
+    def create(cls, path, name, display_name, dim, dtype, device, index_factory=None, spec=None,
+               ivf_factory=None):
         os.makedirs(path, exist_ok=False)
-        st = cls(path, device, index_factory)
+        st = cls(path, device, index_factory, ivf_factory)
         st.name, st.display_name, st.dim, st.dtype = name, display_name, int(dim), dtype
+        st.spec = dict(spec or {"kind": "flat"})
         st.generation = uuid.uuid4().hex
         st.index = st.index_factory(st.dim, dtype, st.device)
         st.version = 0
@@ -179,8 +214,8 @@ class LocalStore:
         return st
 
     @classmethod
-    def open(cls, path, device, index_factory=None):
-        st = cls(path, device, index_factory)
+    def open(cls, path, device, index_factory=None, ivf_factory=None):
+        st = cls(path, device, index_factory, ivf_factory)
         with st.lock:
             st._sync()
         return st
@@ -192,6 +227,9 @@ class LocalStore:
         if self.index is not None:
             self.index.close()
         self.index = self.index_factory(self.dim, self.dtype, self.device)
+        self.spec = man.get("index") or {"kind": "flat"}
+        self.ivf_meta = None
+        self._drop_ivf()
         self.rows, self.files = [], {}
         self.meta_bytes = self.files_bytes = self.tombs = 0
         self.version = -1
@@ -209,6 +247,7 @@ class LocalStore:
         if man["version"] == self.version:
             self._stat = stat
             return
+        self.ivf_meta = man.get("ivf")
         n_rows = int(man["rows"])
         if n_rows < len(self.rows) or man["meta_bytes"] < self.meta_bytes or man["files_bytes"] < self.files_bytes \
                 or man["tombs"] < self.tombs:
@@ -229,6 +268,7 @@ class LocalStore:
         self.meta_bytes, self.files_bytes, self.tombs = man["meta_bytes"], man["files_bytes"], man["tombs"]
         self.version = man["version"]
         self._stat = stat
+        self._ivf_catch_up()
 
     def _apply_file_record(self, r):
         if r["op"] == "add":
@@ -274,8 +314,14 @@ class LocalStore:
             self.files_bytes = _append(self._p("files.jsonl"), self.files_bytes, (json.dumps(rec) + "\n").encode())
             self._apply_file_record(rec)
             self.rows.extend((file_id, c) for c in chunks)
-            self.version += 1
-            self._write_manifest()
+            try:
+                self._maybe_train()
+                self.version += 1
+                self._write_manifest()
+            except BaseException:
+                self._rollback(first)
+                raise
+            self._ivf_catch_up()
             return file_id, first
 
     def _rollback(self, first):
@@ -283,6 +329,81 @@ class LocalStore:
         man, stat = self._read_manifest()
         self.generation = None
         self._sync(man, stat)
+
+    # ---- IVF (config 5) ------------------------------------------------------------------------------
+    def _ivf_enabled(self):
+        return self.spec.get("kind") == "ivf" and getattr(self.index, "supports_ivf", True)
+
+    def _new_ivf(self):
+        if self.ivf_factory is None:
+            from .ivf import IvfIndex
+            LocalStore.ivf_factory = IvfIndex
+        return self.ivf_factory(self.dim, int(self.spec["nlist"]), self.device)
+
+    def _drop_ivf(self):
+        if self.ivf is not None:
+            self.ivf.close()
+        self.ivf = self.ivf_id = None
+
+    def _live_rows(self):
+        ids = [np.arange(f["first"], f["first"] + f["n"], dtype=np.int64)
+               for f in self.files.values() if not f["deleted"] and f["n"]]
+        return np.sort(np.concatenate(ids)) if ids else np.zeros(0, dtype=np.int64)
+
+    def _maybe_train(self):
+        """Writer, under the writer lock, before the manifest commit: train the coarse quantiser
+        when the live rows first reach train_min, and again at every 8x growth since the last
+        training; the centroids file is fsync'ed before the manifest that names it."""
+        if not self._ivf_enabled():
+            return
+        live = self._live_rows()
+        nlist = int(self.spec["nlist"])
+        last = self.ivf_meta["rows"] if self.ivf_meta else 0
+        if live.size < max(int(self.spec["train_min"]), nlist) or (last and live.size < 8 * last):
+            return
+        sample = live[::max(1, live.size // (64 * nlist))]
+        ivf = self._new_ivf()
+        try:
+            ivf.train_from(self.index, sample)
+            raw = ivf.centroid_bytes()
+        except BaseException:
+            ivf.close()
+            raise
+        cid = uuid.uuid4().hex
+        hdr = _CENT_MAGIC + np.array([nlist, self.dim, 0], dtype="<u4").tobytes()
+        tmp = self._p(f"ivf-{cid}.bin.tmp")
+        with open(tmp, "wb") as f:
+            f.write(hdr + raw)
+            f.flush()
+            os.fsync(f.fileno())
+        os.replace(tmp, self._p(f"ivf-{cid}.bin"))
+        _fsync_dir(self.path)
+        self._drop_ivf()
+        self.ivf, self.ivf_id = ivf, cid  # lists are filled by _ivf_catch_up after the commit
+        self.ivf_meta = {"id": cid, "rows": int(live.size)}
+
+    def _ivf_catch_up(self):
+        """Bring this process's IVF lists up to the committed rows (caller holds self.lock)."""
+        if not self._ivf_enabled() or not self.ivf_meta:
+            self._drop_ivf()
+            return
+        cid = self.ivf_meta["id"]
+        if self.ivf_id != cid:
+            self._drop_ivf()
+            with open(self._p(f"ivf-{cid}.bin"), "rb") as f:
+                raw = f.read()
+            nlist = int(self.spec["nlist"])
+            head = np.frombuffer(raw[8:20], dtype="<u4")
+            if raw[:8] != _CENT_MAGIC or int(head[0]) != nlist or int(head[1]) != self.dim \
+                    or len(raw) != 20 + nlist * self.dim:
+                raise RuntimeError(f"{self.path}: centroid file ivf-{cid}.bin is malformed")
+            ivf = self._new_ivf()
+            ivf.load_centroids(raw[20:])
+            self.ivf, self.ivf_id = ivf, cid
+        self.ivf.add_from(self.index, self.index.rows)
+
+    def ivf_ready(self) -> bool:
+        return self.ivf is not None and self.ivf.rows == self.index.rows
 
     def delete_file(self, file_id) -> bool:
         with self.lock, self._WriterLock(self):
@@ -303,6 +424,18 @@ class LocalStore:
             return True
 
     # ---- reads -------------------------------------------------------------------------------------
+    def search(self, queries, k, row_mask=None):
+        """(scores, rows) of the top-k rows per query.  An IVF store with trained lists answers
+        unfiltered searches from its lists (nprobe probes, exact re-rank of min(64, max(16, 2k))
+        candidates); otherwise, and under a metadata filter, the exact scan runs."""
+        if row_mask is None and self.ivf is not None:
+            with self.lock:  # the re-rank reads the DeviceIndex rows in place: no append meanwhile
+                if self.ivf_ready():
+                    s, r = self.ivf.search_index(queries, k, int(self.spec["nprobe"]), self.index,
+                                                 rerank_k=min(64, max(16, 2 * int(k))))
+                    return s.cpu(), r.cpu()
+        return self.index.search(queries, k, row_mask=row_mask)
+
     def row_mask(self, metadata_filter):
         """Device row mask (int32 words) of the live files whose upload metadata matches the
         filter (rfx.filters), or None when no file matches.  Cached per (store version, filter)."""
@@ -333,6 +466,7 @@ class LocalStore:
 
     def close(self):
         with self.lock:
+            self._drop_ivf()
             if self.index is not None:
                 self.index.close()
 
@@ -341,7 +475,7 @@ class StoreRegistry:
     """Process-wide map store name -> LocalStore: lazy open, incremental catch-up when another
     process committed, eviction when another process dropped the store."""
 
-    def __init__(self, root=None, device=None, index_factory=None, devices=None):
+    def __init__(self, root=None, device=None, index_factory=None, devices=None, ivf_factory=None):
         """devices (or RFX_DEVICES, e.g. "0,1,2,3,4,5,6,7"; "0x4" = 4 logical shards on device 0):
         more than one -> every store is row-sharded over them (rfx.sharded.ShardedIndex)."""
         self.root = root or default_root()
@@ -354,6 +488,7 @@ class StoreRegistry:
             if len(devs) > 1:
                 self.device = devs[0]
                 self.index_factory = lambda dim, dtype, device, _d=tuple(devs): ShardedIndex(dim, dtype, list(_d))
+        self.ivf_factory = ivf_factory
         self._stores = {}
         self._lock = threading.Lock()
         self.on_evict = []  # callbacks(name) when a store leaves this registry (rfx.retriever)
@@ -363,10 +498,12 @@ class StoreRegistry:
             return None
         return os.path.join(self.root, name[len(STORE_PREFIX + "local-"):])
 
-    def create(self, display_name, dim, dtype):
+    def create(self, display_name, dim, dtype, spec=None):
+        """spec: the store's index kind (index_spec_from_env() when None)."""
         name = f"{STORE_PREFIX}local-{uuid.uuid4().hex}"
         os.makedirs(self.root, exist_ok=True)
-        st = LocalStore.create(self._dir(name), name, display_name, dim, dtype, self.device, self.index_factory)
+        st = LocalStore.create(self._dir(name), name, display_name, dim, dtype, self.device, self.index_factory,
+                               spec if spec is not None else index_spec_from_env(), self.ivf_factory)
         with self._lock:
             self._stores[name] = st
         return st
@@ -392,7 +529,7 @@ class StoreRegistry:
             if d is None or not os.path.exists(os.path.join(d, "manifest.json")):
                 return None
             try:
-                st = LocalStore.open(d, self.device, self.index_factory)
+                st = LocalStore.open(d, self.device, self.index_factory, self.ivf_factory)
             except StoreGone:
                 return None
             self._stores[name] = st

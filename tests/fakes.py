@@ -157,3 +157,74 @@ class HostIndex:
 
     def close(self):
         self.closed = True
+
+    def read(self, row0, n):
+        """Rows [row0, row0 + n) decoded to f32 (NaN for tombstoned rows)."""
+        d = self.data[row0:row0 + n]
+        if self.dtype == "bf16":
+            return (d.astype(np.uint32) << 16).view(np.float32)
+        return d.astype(np.float32)
+
+
+class HostIvf:
+    """Test-only host stand-in for rfx.ivf.IvfIndex with the interface LocalStore uses (train_from,
+    centroid_bytes / load_centroids, add_from, search_index).  The quantiser is deliberately
+    simple (centroids = the first nlist sampled rows, int8); what the store tests check is the
+    protocol around it: who trains, which centroids every process loads, that lists grow by the
+    appended rows only, and that the re-rank reads the store's rows (tombstones NaN)."""
+
+    log = []  # (op, args) of every call, for the protocol tests
+
+    def __init__(self, dim, nlist, device=0):
+        self.dim, self.nlist = int(dim), int(nlist)
+        self.qc = None
+        self.labels = np.zeros(0, dtype=np.int64)
+        self.closed = False
+
+    @property
+    def rows(self):
+        return self.labels.size
+
+    @staticmethod
+    def _q8(x):
+        a = np.nanmax(np.abs(x), axis=1, keepdims=True)
+        a = np.where(np.isfinite(a) & (a > 0), a, 1.0)
+        return np.clip(np.rint(np.nan_to_num(x) * (127.0 / a)), -127, 127).astype(np.int8)
+
+    def train_from(self, index, row_ids):
+        HostIvf.log.append(("train", len(row_ids)))
+        x = index.read(0, index.rows)[np.asarray(row_ids)]
+        assert not np.isnan(x).any(), "training sample holds tombstoned rows"
+        self.qc = self._q8(x[:self.nlist])
+
+    def centroid_bytes(self):
+        return self.qc.tobytes()
+
+    def load_centroids(self, raw):
+        HostIvf.log.append(("load", len(raw)))
+        self.qc = np.frombuffer(raw, dtype=np.int8).reshape(self.nlist, self.dim).copy()
+
+    def add_from(self, index, upto):
+        if upto > self.rows:
+            HostIvf.log.append(("add", self.rows, upto))
+            x = self._q8(index.read(self.rows, upto - self.rows)).astype(np.int64)
+            self.labels = np.concatenate([self.labels, np.argmax(x @ self.qc.astype(np.int64).T, axis=1)])
+
+    def search_index(self, queries, k, nprobe, index, rerank_k=None):
+        import torch
+        q = np.asarray(queries, dtype=np.float32)
+        x = index.read(0, self.rows)
+        out_s = np.full((len(q), k), -np.inf, dtype=np.float32)
+        out_r = np.full((len(q), k), -1, dtype=np.int64)
+        for i, qi in enumerate(q):
+            probe = np.argsort(-(self.qc.astype(np.float32) @ qi), kind="stable")[:nprobe]
+            cand = np.flatnonzero(np.isin(self.labels, probe))
+            sc = x[cand] @ qi
+            keep = ~np.isnan(sc)
+            cand, sc = cand[keep], sc[keep]
+            order = np.lexsort((cand, -sc))[:k]
+            out_s[i, :len(order)], out_r[i, :len(order)] = sc[order], cand[order]
+        return torch.from_numpy(out_s), torch.from_numpy(out_r)
+
+    def close(self):
+        self.closed = True
