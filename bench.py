@@ -47,6 +47,8 @@ def parse():
     # would otherwise be re-read from the cache (config 2: 307 MB); 0 = enough copies that
     # ~768 MB of other rows pass between two reads of one copy
     ap.add_argument("--copies", type=int, default=0)
+    ap.add_argument("--unfused", action="store_true",
+                    help="VALU plans: time scan and merge as separate launches (A/B of the one-launch search)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     # oracle check of the last timed step (rank 0, N = 1): every `stride`-th query against
     # oracle.search.topk_blocks over ALL rows (read back after the timed region); 0 = off
@@ -145,10 +147,22 @@ def main():
     from rfx import _lib
     from rfx._lib import check, lib, ptr, stream_ptr
 
+    # a VALU plan (nq <= 8) on one GPU runs as ONE launch (rfx_search: scan + last-block merge);
+    # the events then bracket the whole search, merge included
+    fused = world == 1 and kern == 0 and not a.unfused
+    out_s = torch.empty((a.nq, a.k), dtype=torch.float32, device=dev)
+    out_r = torch.empty((a.nq, a.k), dtype=torch.int64, device=dev)
+
     def step(i, ev=None):
         h = ixs[i % copies].handle
         if ev is not None:
             ev[0].record(stream)
+        if fused:
+            check(lib.rfx_search(h, ptr(q), a.nq, a.k, ptr(out_s), ptr(out_r), ptr(ws), ws.numel(),
+                                 stream_ptr(stream)))
+            if ev is not None:
+                ev[1].record(stream)
+            return out_s, out_r
         check(lib.rfx_scan_topk(h, ptr(q), a.nq, a.k, ptr(cs), ptr(cr), ptr(ws), ws.numel(),
                                 stream_ptr(stream)))
         if ev is not None:
@@ -211,7 +225,7 @@ def main():
         "config": {"workload": f"{workload_name(a)}: {a.rows}x{a.dim} {a.dtype} corpus row-sharded over {world} "
                                f"GPU(s), {a.nq} queries/batch, brute-force top-{a.k}",
                    "rows": a.rows, "dim": a.dim, "nq": a.nq, "k": a.k, "parallelism": f"rowshard{world}",
-                   "corpus_copies": copies,
+                   "corpus_copies": copies, "launches_per_step": 1 if fused else 3,
                    "exchange": ("RCCL all-gather from librfx (rfx_allgather_records)" if comm is not None else
                                 "host (gloo) rehearsal" if world > 1 else "none (one shard)"),
                    "scan_kernel": {0: "valu", 1: "mfma128", 2: "mfma256", 3: "mfma_qstationary128",

@@ -1,10 +1,13 @@
-"""IVF-Flat int8 (build plan item 8) — CPU restatement of
-rag-foundation_amd/csrc/k_ivf.hip.  TEST INFRASTRUCTURE ONLY (tests/, smoke(), bench.py's
-cpu_baseline); never imported by the product path.
+"""IVF-Flat int8 (build plan item 8) — the SPECIFICATION of the path's
+numerics, written as plain numpy from the formulas below (a standard IVF-Flat with symmetric
+per-row int8 quantisation and spherical k-means), not from the kernels; the HIP implementation
+(rag-foundation_amd/csrc/k_ivf.hip) is held to it.  TEST INFRASTRUCTURE ONLY (tests/, smoke(),
+bench.py's cpu_baseline); never imported by the product path.
 
 The reference has no IVF (its retrieval runs inside Gemini): SURVEY §8 marks config 5 an extension
-with "no reference counterpart", so this restatement defines the numerics and the GPU path is held
-to it BIT-EXACTLY.  Every step is integer arithmetic or a single correctly rounded f32 operation
+with "no reference counterpart", so parity is UNPINNED against the reference by construction: this
+file defines the numerics and the GPU path is held to it BIT-EXACTLY.  The names in parentheses
+below say which kernel implements each step.  Every step is integer arithmetic or a single correctly rounded f32 operation
 (IEEE in numpy and via the __f*_rn intrinsics on the GPU), so there is no tolerance anywhere:
 
   quantize (rows and queries; k_ivf.hip quantize_kernel)

@@ -97,13 +97,75 @@ __device__ __forceinline__ float elem(const uint4& v, int e) {
   }
 }
 
-template <int DT, int NQT, int K, int VPL>
+struct MergeRec {  // 16 B; the layout of rfx/dist.py pack(): int64(score bits) + int64 row
+  float s;
+  int pad;
+  long long r;
+};
+
+template <bool R64>
+struct FlatSrc {
+  const float* cs;
+  const void* cr;
+  int64_t n;  // candidates per query
+  __device__ __forceinline__ void get(int64_t q, int64_t i, float& s, long long& r) const {
+    s = cs[q * n + i];
+    if constexpr (R64)
+      r = ((const long long*)cr)[q * n + i];
+    else
+      r = (long long)((const int*)cr)[q * n + i];
+  }
+};
+struct GatheredSrc {
+  const MergeRec* rec;
+  int64_t nq;
+  int k;  // entries per rank (= list_len)
+  int64_t n;
+  __device__ __forceinline__ void get(int64_t q, int64_t i, float& s, long long& r) const {
+    const int ii = (int)i;  // n_cand < 2^31 (host check)
+    const int64_t rank = ii / k, e = ii - (ii / k) * k;
+    const MergeRec m = rec[(rank * nq + q) * k + e];
+    s = m.s;
+    r = m.r;
+  }
+};
+
+constexpr long long kNoRow = 0x7fffffffffffffffll;
+
+// FUSED (the whole search in one launch, rfx_search on a VALU plan): the queries are read in the
+// index dtype and widened here (no widen kernel), and the last block of each query slice to finish
+// (agent-scope release/acquire on a per-slice counter) merges the slice's candidates into the final
+// top-k (no merge launch), then returns the launch state (bounds, counter) to zero for the next
+// search on the same stream.  `Qf` is then the raw [nq][D] query buffer in dtype DT.
+struct FusedOut {
+  uint32_t* ctr;  // [q_slices] arrival counters (zero on entry, left zero)
+  int k_out;
+  float* out_s;
+  int64_t* out_r;
+};
+
+template <int DT>
+__device__ __forceinline__ float query_elem(const void* Q, int64_t i) {
+  if constexpr (DT == RFX_F32)
+    return ((const float*)Q)[i];
+  else if constexpr (DT == RFX_BF16)
+    return bf16_to_f32(((const uint16_t*)Q)[i]);
+  else
+    return f16_to_f32(((const uint16_t*)Q)[i]);
+}
+
+template <int K, bool R64, int NW, class Src>
+__device__ __forceinline__ void merge_one(const Src& src, int64_t q, int list_len, int k_out, int64_t row_offset,
+                                          float* __restrict__ out_s, int64_t* __restrict__ out_r,
+                                          MergeRec* __restrict__ out_rec);
+
+template <int DT, int NQT, int K, int VPL, bool FUSED>
 __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restrict__ X, int nrows, int D,
-                                                        const float* __restrict__ Qf, int nq,
+                                                        const void* __restrict__ Qf, int nq,
                                                         int rows_per_wave, float* __restrict__ cand_s,
                                                         int* __restrict__ cand_r, int n_lists,
                                                         const uint32_t* __restrict__ mask,
-                                                        uint32_t* __restrict__ tau) {
+                                                        uint32_t* __restrict__ tau, FusedOut fo) {
   constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
   constexpr int EPV = 16 / ESZ;
   extern __shared__ __attribute__((aligned(16))) float q_lds[];  // [NQT][D]
@@ -113,7 +175,8 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
   const int nqt = min(NQT, nq - q0);
   for (int i = tid; i < NQT * D; i += 256) {
     const int qi = i / D;
-    q_lds[i] = qi < nqt ? Qf[(int64_t)(q0 + qi) * D + (i - qi * D)] : 0.f;
+    const int64_t src = (int64_t)(q0 + qi) * D + (i - qi * D);
+    q_lds[i] = qi >= nqt ? 0.f : FUSED ? query_elem<DT>(Qf, src) : ((const float*)Qf)[src];
   }
   __syncthreads();
 
@@ -223,6 +286,26 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
       cand_r[o] = keep ? M.lr : kEmptyRow;
     }
   }
+  if constexpr (FUSED) {
+    __shared__ int last;
+    __threadfence();  // release: this block's candidates and bounds, before it is counted
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t old =
+          __hip_atomic_fetch_add(fo.ctr + blockIdx.y, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      last = old == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();  // acquire: every block of the slice has published its candidates
+    const FlatSrc<false> src{cand_s, cand_r, (int64_t)n_lists * K};
+    for (int qi = 0; qi < nqt; ++qi) {
+      merge_one<K, false, 4>(src, q0 + qi, K, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
+      __syncthreads();
+    }
+    if (tid < nqt && tau) tau[q0 + tid] = 0u;  // every block's bound updates precede its arrival
+    if (tid == 0) fo.ctr[blockIdx.y] = 0u;
+  }
 }
 
 // K values instantiated for the scan; runtime k is rounded up to one of these and only the
@@ -231,13 +314,17 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
 
 template <int DT, int NQT, int K>
 static int launch_valu_vpl(int vpl, dim3 grid, size_t lds, hipStream_t st, const uint8_t* X, int nrows,
-                           int D, const float* Qf, int nq, int rpw, float* cs, int* cr, int n_lists,
-                           const uint32_t* mask, uint32_t* tau) {
-#define RFX_L(V)                                                                                  \
-  if (vpl <= V) {                                                                                 \
-    hipLaunchKernelGGL((scan_valu_kernel<DT, NQT, K, V>), grid, dim3(256), lds, st, X, nrows, D, Qf, \
-                       nq, rpw, cs, cr, n_lists, mask, tau);                                      \
-    return 0;                                                                                     \
+                           int D, const void* Qf, int nq, int rpw, float* cs, int* cr, int n_lists,
+                           const uint32_t* mask, uint32_t* tau, const FusedOut& fo) {
+#define RFX_L(V)                                                                                       \
+  if (vpl <= V) {                                                                                      \
+    if (fo.ctr)                                                                                        \
+      hipLaunchKernelGGL((scan_valu_kernel<DT, NQT, K, V, true>), grid, dim3(256), lds, st, X, nrows, D, \
+                         Qf, nq, rpw, cs, cr, n_lists, mask, tau, fo);                                 \
+    else                                                                                               \
+      hipLaunchKernelGGL((scan_valu_kernel<DT, NQT, K, V, false>), grid, dim3(256), lds, st, X, nrows,   \
+                         D, Qf, nq, rpw, cs, cr, n_lists, mask, tau, fo);                              \
+    return 0;                                                                                          \
   }
   RFX_L(4) RFX_L(8) RFX_L(12) RFX_L(16)
 #undef RFX_L
@@ -246,10 +333,10 @@ static int launch_valu_vpl(int vpl, dim3 grid, size_t lds, hipStream_t st, const
 
 template <int DT, int NQT>
 static int launch_valu_k(int kk, int vpl, dim3 grid, size_t lds, hipStream_t st, const uint8_t* X,
-                         int nrows, int D, const float* Qf, int nq, int rpw, float* cs, int* cr,
-                         int n_lists, const uint32_t* mask, uint32_t* tau) {
+                         int nrows, int D, const void* Qf, int nq, int rpw, float* cs, int* cr,
+                         int n_lists, const uint32_t* mask, uint32_t* tau, const FusedOut& fo) {
 #define RFX_K(KV) \
-  if (kk == KV) return launch_valu_vpl<DT, NQT, KV>(vpl, grid, lds, st, X, nrows, D, Qf, nq, rpw, cs, cr, n_lists, mask, tau);
+  if (kk == KV) return launch_valu_vpl<DT, NQT, KV>(vpl, grid, lds, st, X, nrows, D, Qf, nq, rpw, cs, cr, n_lists, mask, tau, fo);
   RFX_VALU_K_LIST(RFX_K)
 #undef RFX_K
   return -1;
@@ -283,8 +370,8 @@ ValuPlan plan_scan_valu(int64_t nrows, int D, int dtype, int64_t nq, int k) {
   return p;
 }
 
-int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dtype, const float* Qf,
-                     int nq, float* cs, int* cr, hipStream_t st, const uint32_t* mask, uint32_t* tau) {
+static int launch_valu(const ValuPlan& p, const void* X, int nrows, int D, int dtype, const void* Qf, int nq,
+                       float* cs, int* cr, hipStream_t st, const uint32_t* mask, uint32_t* tau, const FusedOut& fo) {
   dim3 grid(p.blocks, p.q_slices);
   const size_t lds = (size_t)p.nqt * D * sizeof(float);
   const uint8_t* Xb = (const uint8_t*)X;
@@ -292,16 +379,29 @@ int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dty
   if (p.nqt == NQV) {                                                                              \
     if (dtype == RFX_F32)                                                                          \
       return launch_valu_k<RFX_F32, NQV>(p.k_slot, p.vpl, grid, lds, st, Xb, nrows, D, Qf, nq,       \
-                                         p.rows_per_wave, cs, cr, p.n_lists, mask, tau);                      \
+                                         p.rows_per_wave, cs, cr, p.n_lists, mask, tau, fo);                  \
     if (dtype == RFX_BF16)                                                                         \
       return launch_valu_k<RFX_BF16, NQV>(p.k_slot, p.vpl, grid, lds, st, Xb, nrows, D, Qf, nq,      \
-                                          p.rows_per_wave, cs, cr, p.n_lists, mask, tau);                     \
+                                          p.rows_per_wave, cs, cr, p.n_lists, mask, tau, fo);                 \
     return launch_valu_k<RFX_F16, NQV>(p.k_slot, p.vpl, grid, lds, st, Xb, nrows, D, Qf, nq,         \
-                                       p.rows_per_wave, cs, cr, p.n_lists, mask, tau);                        \
+                                       p.rows_per_wave, cs, cr, p.n_lists, mask, tau, fo);                    \
   }
   RFX_NQ(1) RFX_NQ(4) RFX_NQ(8)
 #undef RFX_NQ
   return -1;
+}
+
+int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dtype, const float* Qf, int nq,
+                     float* cs, int* cr, hipStream_t st, const uint32_t* mask, uint32_t* tau) {
+  return launch_valu(p, X, nrows, D, dtype, Qf, nq, cs, cr, st, mask, tau, FusedOut{nullptr, 0, nullptr, nullptr});
+}
+
+int launch_search_valu_fused(const ValuPlan& p, const void* X, int nrows, int D, int dtype, const void* Q, int nq,
+                             float* cs, int* cr, uint32_t* state, int k, float* out_s, int64_t* out_r,
+                             hipStream_t st, const uint32_t* mask) {
+  // state: [kFusedMaxNq] bounds then [q_slices] counters, all zero (and left zero)
+  return launch_valu(p, X, nrows, D, dtype, Q, nq, cs, cr, st, mask, state,
+                     FusedOut{state + kValuFusedMaxNq, k, out_s, out_r});
 }
 
 // Diagnostic streaming read (HBM ceiling calibration): every byte read once with dwordx4.
@@ -350,55 +450,20 @@ void launch_widen_queries(const void* Q, int64_t n, int dtype, float* out, hipSt
 // Sources: flat [nq][n_cand] (score, row) arrays, or the all-gathered per-rank records of the
 // multi-GPU path ([world][nq][k] of {f32 score, pad, i64 row}).
 // ---------------------------------------------------------------------------------------
-struct MergeRec {  // 16 B; the layout of rfx/dist.py pack(): int64(score bits) + int64 row
-  float s;
-  int pad;
-  long long r;
-};
 
-template <bool R64>
-struct FlatSrc {
-  const float* cs;
-  const void* cr;
-  int64_t n;  // candidates per query
-  __device__ __forceinline__ void get(int64_t q, int64_t i, float& s, long long& r) const {
-    s = cs[q * n + i];
-    if constexpr (R64)
-      r = ((const long long*)cr)[q * n + i];
-    else
-      r = (long long)((const int*)cr)[q * n + i];
-  }
-};
-struct GatheredSrc {
-  const MergeRec* rec;
-  int64_t nq;
-  int k;  // entries per rank (= list_len)
-  int64_t n;
-  __device__ __forceinline__ void get(int64_t q, int64_t i, float& s, long long& r) const {
-    const int ii = (int)i;  // n_cand < 2^31 (host check)
-    const int64_t rank = ii / k, e = ii - (ii / k) * k;
-    const MergeRec m = rec[(rank * nq + q) * k + e];
-    s = m.s;
-    r = m.r;
-  }
-};
-
-constexpr long long kNoRow = 0x7fffffffffffffffll;
-
-// Fold candidates i = base + (p * 8 * 64) + lane, p < P, of one query into the wave list.  All P
+// Fold candidates i = base + (p * NW * 64) + lane, p < P, of one query into the wave list.  All P
 // loads are issued before the first offer, so a chunk costs one memory latency, not P.
-// `skip_heads`: candidates at list heads (i % list_len == 0) are not offered.
-template <int K, bool R64, int P, class Src>
+template <int K, bool R64, int P, int NW, class Src>
 __device__ __forceinline__ void merge_chunk(const Src& src, int64_t q, int64_t base, int64_t n, int lane,
-                                            int list_len, bool skip_heads, WaveList64<K>& L) {
+                                            WaveList64<K>& L) {
   float sc[P];
   long long rr[P];
 #pragma unroll
   for (int p = 0; p < P; ++p) {
-    const int64_t i = base + (int64_t)p * 8 * 64 + lane;
+    const int64_t i = base + (int64_t)p * NW * 64 + lane;
     sc[p] = -__builtin_inff();
     rr[p] = kNoRow;
-    if (i < n && !(skip_heads && (int)i % list_len == 0)) src.get(q, i, sc[p], rr[p]);  // (n < 2^31)
+    if (i < n) src.get(q, i, sc[p], rr[p]);  // (n < 2^31)
   }
 #pragma unroll
   for (int p = 0; p < P; ++p) {
@@ -441,20 +506,22 @@ __device__ __forceinline__ void rank_merge(const float (*ls)[K], const long long
   }
 }
 
-template <int K, bool R64, class Src>
-__global__ __launch_bounds__(512) void merge_kernel(Src src, int list_len, int k_out, int64_t row_offset,
-                                                    float* __restrict__ out_s, int64_t* __restrict__ out_r,
-                                                    MergeRec* __restrict__ out_rec) {
-  // rows 0..7: wave lists, row 8: H (top-K of pass 1), row 9: final
-  __shared__ float ls_lds[10][K];
-  __shared__ long long lr_lds[10][K];
-  const int64_t q = blockIdx.x;
+// One query's merge by a block of NW waves (the merge kernel: NW = 8; the fused single-launch
+// VALU search's last block: NW = 4).
+template <int K, bool R64, int NW, class Src>
+__device__ __forceinline__ void merge_one(const Src& src, int64_t q, int list_len, int k_out, int64_t row_offset,
+                                          float* __restrict__ out_s, int64_t* __restrict__ out_r,
+                                          MergeRec* __restrict__ out_rec) {
+  constexpr int NT = NW * 64;
+  // rows 0..NW-1: wave lists, row NW: the final list
+  __shared__ float ls_lds[NW + 1][K];
+  __shared__ long long lr_lds[NW + 1][K];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int64_t n = src.n;
-  constexpr int P = 8;  // chunk: 8 * 512 candidates per block
-  if (tid < 2 * K) {
-    ls_lds[8 + tid / K][tid % K] = -__builtin_inff();
-    lr_lds[8 + tid / K][tid % K] = kNoRow;
+  constexpr int P = 8;  // chunk: 8 * NT candidates per block
+  if (tid < K) {
+    ls_lds[NW][tid] = -__builtin_inff();
+    lr_lds[NW][tid] = kNoRow;
   }
   // ---- bound: with lists of list_len >= k_out entries, the minimum of a list's first k_out
   // entries is a lower bound of the query's k_out-th best (that list alone holds k_out candidates
@@ -472,20 +539,23 @@ __global__ __launch_bounds__(512) void merge_kernel(Src src, int list_len, int k
   uint32_t* hk = (uint32_t*)hk4;
   const int64_t n_heads64 = n / list_len;
   const int nh = (int)(n_heads64 < 512 ? n_heads64 : 512);
-  uint32_t mine = 0u;
+  uint32_t mine[512 / NT];
   if (tid == 0) tb = 0u;
-  if (tid < 512) {
-    if (tid < nh) {
+#pragma unroll
+  for (int u = 0; u < 512 / NT; ++u) {
+    const int h = tid + u * NT;
+    mine[u] = 0u;
+    if (h < nh) {
       float hs;
       long long hr;
-      src.get(q, (int64_t)tid * list_len, hs, hr);
+      src.get(q, (int64_t)h * list_len, hs, hr);
       const bool live = hr >= 0 && hr != kNoRow && (R64 || hr != (long long)kEmptyRow);
-      mine = live ? ord_f32(hs) : 0u;
+      mine[u] = live ? ord_f32(hs) : 0u;
     }
   }
   uint32_t m = 0u;  // list bound (below), reduced after the barrier
   if (list_len > 1 && list_len >= k_out) {
-    for (int64_t j = tid; j < n / list_len; j += 512) {
+    for (int64_t j = tid; j < n / list_len; j += NT) {
       uint32_t mj = 0xffffffffu;  // min over the list's first k_out entries (sorted or not)
       for (int e0 = 0; e0 < k_out; e0 += 8) {  // 8 independent loads in flight per round
         float sc[8];
@@ -507,17 +577,21 @@ __global__ __launch_bounds__(512) void merge_kernel(Src src, int list_len, int k
 #pragma unroll
     for (int off = 32; off; off >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, off));
   }
-  if (tid < 512) hk[tid] = mine;  // after the list pass, so its loads overlap the head load
+#pragma unroll
+  for (int u = 0; u < 512 / NT; ++u) hk[tid + u * NT] = mine[u];  // after the list pass: loads overlap
   __syncthreads();
   if (nh >= k_out) {
     uint32_t cand = 0u;
-    if (mine) {
-      int c = 0;
-      for (int i = 0; i < (nh + 3) / 4; ++i) {
-        const uint4 v = hk4[i];
-        c += (v.x >= mine) + (v.y >= mine) + (v.z >= mine) + (v.w >= mine);
+#pragma unroll
+    for (int u = 0; u < 512 / NT; ++u) {
+      if (mine[u]) {
+        int c = 0;
+        for (int i = 0; i < (nh + 3) / 4; ++i) {
+          const uint4 v = hk4[i];
+          c += (v.x >= mine[u]) + (v.y >= mine[u]) + (v.z >= mine[u]) + (v.w >= mine[u]);
+        }
+        if (c >= k_out) cand = max(cand, mine[u]);
       }
-      cand = c >= k_out ? mine : 0u;
     }
 #pragma unroll
     for (int off = 32; off; off >>= 1) cand = max(cand, (uint32_t)__shfl_xor((int)cand, off));
@@ -529,20 +603,19 @@ __global__ __launch_bounds__(512) void merge_kernel(Src src, int list_len, int k
     const uint32_t u = tb & 0x80000000u ? tb & 0x7fffffffu : ~tb;  // inverse of ord_f32
     L.init_above(__uint_as_float(u), kNoRow);                      // admits score >= T
   }
-  for (int64_t base = (int64_t)w * 64; base < n; base += (int64_t)P * 8 * 64)
-    merge_chunk<K, R64, P>(src, q, base, n, lane, 1, false, L);
+  for (int64_t base = (int64_t)w * 64; base < n; base += (int64_t)P * NW * 64)
+    merge_chunk<K, R64, P, NW>(src, q, base, n, lane, L);
   if (lane < K) {
     ls_lds[w][lane] = L.ls;
     lr_lds[w][lane] = L.lr;
   }
   __syncthreads();
-  rank_merge<K, 8>(ls_lds, lr_lds, ls_lds[8], lr_lds[8]);
+  rank_merge<K, NW>(ls_lds, lr_lds, ls_lds[NW], lr_lds[NW]);
   __syncthreads();
-  const int fin = 8;
   if (tid < k_out) {
-    const long long rr = lr_lds[fin][tid];
+    const long long rr = lr_lds[NW][tid];
     const bool empty = rr == kNoRow;
-    const float s = empty ? -__builtin_inff() : ls_lds[fin][tid];
+    const float s = empty ? -__builtin_inff() : ls_lds[NW][tid];
     const long long r = empty ? -1 : rr + row_offset;
     if (out_rec) {
       out_rec[q * k_out + tid] = MergeRec{s, 0, r};
@@ -551,6 +624,13 @@ __global__ __launch_bounds__(512) void merge_kernel(Src src, int list_len, int k
       out_r[q * k_out + tid] = r;
     }
   }
+}
+
+template <int K, bool R64, class Src>
+__global__ __launch_bounds__(512) void merge_kernel(Src src, int list_len, int k_out, int64_t row_offset,
+                                                    float* __restrict__ out_s, int64_t* __restrict__ out_r,
+                                                    MergeRec* __restrict__ out_rec) {
+  merge_one<K, R64, 8>(src, (int64_t)blockIdx.x, list_len, k_out, row_offset, out_s, out_r, out_rec);
 }
 
 int launch_topk_merge_lists(const float* cs, const void* cr, int rows_are_i64, int64_t nq, int64_t n_cand,

@@ -64,8 +64,36 @@ struct Index {
   void* data = nullptr;
   std::vector<uint8_t> tomb;  // host bitmap (1 = deleted), mirrors the NaN rows on device
   std::shared_timed_mutex mu;
+  // per-stream launch state of the single-launch VALU search (zeroed once, left zero by every
+  // launch); keyed by stream so concurrent searches on different streams never share it
+  std::mutex state_mu;
+  std::map<hipStream_t, uint32_t*> fused_state;
   int64_t row_bytes() const { return (int64_t)dim * esize(dtype); }
 };
+
+int fused_state(Index& ix, hipStream_t st, uint32_t** out) {
+  std::lock_guard<std::mutex> lk(ix.state_mu);
+  auto it = ix.fused_state.find(st);
+  if (it != ix.fused_state.end()) {
+    *out = it->second;
+    return RFX_OK;
+  }
+  uint32_t* p = nullptr;
+  const size_t bytes = (size_t)rfx::kValuFusedStateWords * 4;
+  if (hipMalloc(&p, bytes) != hipSuccess) return fail(RFX_ENOMEM, "hipMalloc(%zu) failed (search state)", bytes);
+  RFX_HIP(hipMemset(p, 0, bytes));  // synchronous: zero before the first launch on any stream
+  ix.fused_state[st] = p;
+  *out = p;
+  return RFX_OK;
+}
+
+bool fused_enabled() {  // RFX_VALU_FUSED=0: the three-launch path (widen, scan, merge), for A/B runs
+  static const bool on = [] {
+    const char* e = getenv("RFX_VALU_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 // Bounded lock waits: a writer stuck behind long searches (or the reverse) gets RFX_EBUSY, which
 // the host maps to a TimeoutError so the reference's retry paths apply (gemini_rag.py:17-27,
@@ -330,11 +358,13 @@ int rfx_index_destroy(rfx_index_t h) {
     g_reg.erase(it);
   }
   std::unique_lock<std::shared_timed_mutex> lk(ix->mu);  // waits for in-flight searches: never EBUSY
+  RFX_HIP(hipSetDevice(ix->device));
   if (ix->data) {
-    RFX_HIP(hipSetDevice(ix->device));
     RFX_HIP(hipFree(ix->data));
     ix->data = nullptr;
   }
+  for (auto& kv : ix->fused_state) RFX_HIP(hipFree(kv.second));
+  ix->fused_state.clear();
   return RFX_OK;
 }
 
@@ -830,6 +860,15 @@ int rfx_search_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k, c
   uint8_t* ws = (uint8_t*)ws_d;
   float* cs = (float*)(ws + L.cs_off);
   int32_t* cr = (int32_t*)(ws + L.cr_off);
+  if (L.kernel == 0 && ix->rows > 0 && nq > 0 && nq <= rfx::kValuFusedMaxNq && fused_enabled()) {
+    uint32_t* state = nullptr;
+    if ((rc = fused_state(*ix, st, &state))) return rc;
+    if (rfx::launch_search_valu_fused(L.vp, ix->data, (int)ix->rows, ix->dim, ix->dtype, queries_d, (int)nq, cs, cr,
+                                      state, k, out_scores_d, out_rows_d, st, row_mask_d) != 0)
+      return fail(RFX_EUNSUPPORTED, "VALU search launch rejected");
+    RFX_HIP(hipGetLastError());
+    return RFX_OK;
+  }
   rc = scan_into(*ix, L, queries_d, nq, cs, cr, ws, st, row_mask_d);
   if (rc) return rc;
   // the scan's candidates are sorted lists: the merge bounds admission by the lists' k-th entries

@@ -31,6 +31,15 @@ ValuPlan plan_scan_valu(int64_t nrows, int D, int dtype, int64_t nq, int k);
 int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dtype, const float* Qf,
                      int nq, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr,
                      uint32_t* tau = nullptr);
+// The whole search (scan + final merge) in one launch for a VALU plan with nq <= kValuFusedMaxNq:
+// Q is the raw [nq][D] query buffer in the index dtype; state = kValuFusedMaxNq bounds followed by
+// p.q_slices arrival counters, ALL ZERO on entry — the kernel leaves them zero again, so a state
+// buffer zeroed once serves every later search on one stream (rfx_api.hip keeps one per stream).
+constexpr int kValuFusedMaxNq = 1024;
+constexpr int kValuFusedStateWords = kValuFusedMaxNq + 1024;
+int launch_search_valu_fused(const ValuPlan& p, const void* X, int nrows, int D, int dtype, const void* Q, int nq,
+                             float* cs, int* cr, uint32_t* state, int k, float* out_s, int64_t* out_r,
+                             hipStream_t st, const uint32_t* mask = nullptr);
 
 // ---- MFMA scan (batched bf16 / f16) -------------------------------------------------------
 struct MfmaPlan {

@@ -36,7 +36,8 @@ def test_ivf_store_train_search_reader(tmp_path):
     fids = []
     for i, v in enumerate(docs[:3]):
         fids.append(st.add_document([f"d{i}-{j}" for j in range(1500)], v, f"d{i}.md", {"tenant": f"t{i}"})[0])
-    st.delete_file(fids[1])
+        if i == 1:
+            st.delete_file(fids[1])
     assert st.ivf is None  # 3000 live rows < train_min
     st.add_document([f"d3-{j}" for j in range(1500)], docs[3], "d3.md")
     assert st.ivf_ready() and st.ivf_meta["rows"] == 4500

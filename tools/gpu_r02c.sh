@@ -29,3 +29,16 @@ timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmcf" 
 step write
 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$O/pmcw" -o pmcw -- $B --steps 4 --warmup 1 > "$O/bench_pmcw.log" 2>&1 || { tail -20 "$O/bench_pmcw.log"; exit 1; }
 step done
+cd "$R" || exit 1
+if [ -n "$CFG2" ]; then
+step cfg2
+C2="--rows 100000 --dim 768 --dtype f32 --nq 1 --steps 3000 --warmup 200"
+timeout -k 10 300 python -u bench.py $C2 > "$O/bench_cfg2.log" 2>&1 || { tail -20 "$O/bench_cfg2.log"; exit 1; }
+tail -1 "$O/bench_cfg2.log" | cut -c1-300
+timeout -k 10 300 python -u bench.py $C2 --unfused --no-cpu-baseline > "$O/bench_cfg2_unfused.log" 2>&1 || { tail -20 "$O/bench_cfg2_unfused.log"; exit 1; }
+tail -1 "$O/bench_cfg2_unfused.log" | cut -c1-300
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt2" -o kt2 -- python "$R/bench.py" $C2 --no-cpu-baseline --oracle-stride 0 > "$O/bench_kt2.log" 2>&1 || { tail -20 "$O/bench_kt2.log"; exit 1; }
+timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmcf2" -o pmcf2 -- python "$R/bench.py" --rows 100000 --dim 768 --dtype f32 --nq 1 --steps 50 --warmup 10 --no-cpu-baseline --oracle-stride 0 > "$O/bench_pmcf2.log" 2>&1 || { tail -20 "$O/bench_pmcf2.log"; exit 1; }
+step cfg2done
+fi
