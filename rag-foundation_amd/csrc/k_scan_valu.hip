@@ -132,6 +132,18 @@ struct GatheredSrc {
 
 constexpr long long kNoRow = 0x7fffffffffffffffll;
 
+// [nq][n] candidates read with agent-scope loads (sc1): the one-launch search's last block reads
+// what the other blocks of its slice stored the same way during the launch.
+struct AgentSrc {
+  const float* cs;
+  const int* cr;
+  int64_t n;
+  __device__ __forceinline__ void get(int64_t q, int64_t i, float& s, long long& r) const {
+    s = __uint_as_float(__hip_atomic_load((const uint32_t*)cs + q * n + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    r = (long long)__hip_atomic_load(cr + q * n + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+};
+
 // FUSED (the whole search in one launch, rfx_search on a VALU plan): the queries are read in the
 // index dtype and widened here (no widen kernel), and the last block of each query slice to finish
 // (agent-scope release/acquire on a per-slice counter) merges the slice's candidates into the final
@@ -282,23 +294,34 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
     if (lane < K) {
       const int64_t o = ((int64_t)(q0 + qi) * n_lists + blockIdx.x) * K + lane;
       const bool keep = M.lr != kEmptyRow && ord_f32(M.ls) >= bound;
-      cand_s[o] = keep ? M.ls : -__builtin_inff();
-      cand_r[o] = keep ? M.lr : kEmptyRow;
+      const float cs_v = keep ? M.ls : -__builtin_inff();
+      const int cr_v = keep ? M.lr : kEmptyRow;
+      if constexpr (FUSED) {  // agent-coherent stores (sc1): the slice's last block reads them
+        __hip_atomic_store((uint32_t*)cand_s + o, __float_as_uint(cs_v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cand_r + o, cr_v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        cand_s[o] = cs_v;
+        cand_r[o] = cr_v;
+      }
     }
   }
   if constexpr (FUSED) {
+    // Hand-off without cache maintenance: the candidates went out as agent-scope (sc1) stores, so
+    // once every lane's stores are acknowledged (vmcnt 0) they are visible at the device's
+    // coherence point; the arrival counter is an agent-scope atomic, and the last block reads
+    // the candidates with agent-scope loads.  (A release/acquire fence pair here writes back and
+    // invalidates the XCD's whole L2 in every block: measured 1.6x slower at config 2.)
     __shared__ int last;
-    __threadfence();  // release: this block's candidates and bounds, before it is counted
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
       const uint32_t old =
-          __hip_atomic_fetch_add(fo.ctr + blockIdx.y, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(fo.ctr + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       last = old == gridDim.x - 1;
     }
     __syncthreads();
     if (!last) return;
-    __threadfence();  // acquire: every block of the slice has published its candidates
-    const FlatSrc<false> src{cand_s, cand_r, (int64_t)n_lists * K};
+    const AgentSrc src{cand_s, cand_r, (int64_t)n_lists * K};
     for (int qi = 0; qi < nqt; ++qi) {
       merge_one<K, false, 4>(src, q0 + qi, K, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
       __syncthreads();
@@ -352,14 +375,22 @@ ValuPlan plan_scan_valu(int64_t nrows, int D, int dtype, int64_t nq, int k) {
   p.k_slot = valu_k_slot(k);
   p.nqt = nq <= 1 ? 1 : (nq <= 4 ? 4 : 8);
   p.q_slices = (int)((nq + p.nqt - 1) / p.nqt);
-  const int64_t target_waves = 4096;
-  int64_t rpw = (nrows + target_waves - 1) / target_waves;
-  static const int rpw_env = [] {  // RFX_VALU_RPW: ablation override of rows per wave
+  // Blocks: about kValuBlocks (2 per CU), so that every CU streams the same share of the store — a
+  // count just above a multiple of the CU count leaves most CUs idle for the last round (config 2
+  // had 391 blocks on 256 CUs).  Rows per wave: a multiple of 4 (one row per 16-lane group and
+  // iteration), at least 16.
+  static const int blocks_env = [] {  // RFX_VALU_BLOCKS / RFX_VALU_RPW: ablation overrides
+    const char* e = getenv("RFX_VALU_BLOCKS");
+    return e ? atoi(e) : 0;
+  }();
+  static const int rpw_env = [] {
     const char* e = getenv("RFX_VALU_RPW");
     return e ? atoi(e) : 0;
   }();
-  if (rpw < 64) rpw = 64;
-  rpw = (rpw + 63) / 64 * 64;
+  const int64_t target_waves = 4 * (int64_t)(blocks_env > 0 ? blocks_env : kValuBlocks);
+  int64_t rpw = (nrows + target_waves - 1) / target_waves;
+  if (rpw < 16) rpw = 16;
+  rpw = (rpw + 3) / 4 * 4;
   if (rpw_env >= 4) rpw = rpw_env / 4 * 4;
   int64_t waves = (nrows + rpw - 1) / rpw;
   if (waves < 1) waves = 1;
