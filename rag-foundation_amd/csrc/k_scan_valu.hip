@@ -217,46 +217,59 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
 #pragma unroll
   for (int qi = 0; qi < NQT; ++qi) cand[qi] = 0.f;
 
-  for (int base = wb; base < we; base += 64) {
-#pragma unroll 2
-    for (int it = 0; it < 16; ++it) {
-      const int row = base + it * 4 + g;
-      const bool valid = row < we;
-      const uint8_t* rp = X + (int64_t)(valid ? row : wb) * RB;
-      uint4 v[VPL];
+  // Row stream, software-pipelined: iteration t covers rows wb + 64 (t >> 4) + 4 (t & 15) + g (one
+  // row per 16-lane group); the loads of iteration t + 1 are in flight while iteration t computes,
+  // so a wave never drains its loads at a loop back-edge (with one or two waves per SIMD nothing
+  // else hides that latency).  Rows past `we` re-read row wb (cache hits) and are never offered.
+  auto load_row = [&](int t, uint4 (&v)[VPL]) {
+    const int row = wb + 64 * (t >> 4) + 4 * (t & 15) + g;
+    const uint8_t* rp = X + (int64_t)(row < we ? row : wb) * RB;
+    // unconditional loads (clamped address, zeroed by a select): no branch around a load, so
+    // the compiler counts vmcnt per buffer instead of draining at every branch join
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int vv = j + 16 * i;
+      const uint4 x = *(const uint4*)(rp + (int64_t)(vv < VPR ? vv : VPR - 1) * 16);
+      const uint32_t m = vv < VPR ? 0xffffffffu : 0u;  // AND, not a select (which becomes a branch)
+      v[i] = make_uint4(x.x & m, x.y & m, x.z & m, x.w & m);
+    }
+  };
+  auto score_row = [&](int it, const uint4 (&v)[VPL]) {
+#pragma unroll
+    for (int qi = 0; qi < NQT; ++qi) {
+      float acc = 0.f;
 #pragma unroll
       for (int i = 0; i < VPL; ++i) {
-        const int vv = j + 16 * i;
-        if (16 * i < VPR && vv < VPR)
-          v[i] = *(const uint4*)(rp + (int64_t)vv * 16);
-        else
-          v[i] = make_uint4(0, 0, 0, 0);
-      }
+        if (16 * i >= VPR) continue;
 #pragma unroll
-      for (int qi = 0; qi < NQT; ++qi) {
-        float acc = 0.f;
-#pragma unroll
-        for (int i = 0; i < VPL; ++i) {
-          if (16 * i >= VPR) continue;
-#pragma unroll
-          for (int e = 0; e < EPV; ++e) {
-            float qv;
-            if constexpr (NQT == 1)
-              qv = qr[i * EPV + e];
-            else
-              qv = (j + 16 * i < VPR) ? q_lds[qi * D + (j + 16 * i) * EPV + e] : 0.f;
-            acc = fmaf(elem<DT>(v[i], e), qv, acc);
-          }
+        for (int e = 0; e < EPV; ++e) {
+          float qv;
+          if constexpr (NQT == 1)
+            qv = qr[i * EPV + e];
+          else
+            qv = (j + 16 * i < VPR) ? q_lds[qi * D + (j + 16 * i) * EPV + e] : 0.f;
+          acc = fmaf(elem<DT>(v[i], e), qv, acc);
         }
-        acc = row16_sum(acc);
-        if (j == it) cand[qi] = acc;
       }
+      acc = row16_sum(acc);
+      if (j == it) cand[qi] = acc;
     }
-    const int crow = base + j * 4 + g;
-    // metadata filter: rows whose mask bit is clear are never offered
-    const bool ok = crow < we && (mask == nullptr || row_allowed(mask, crow));
+  };
+  const int T = we > wb ? (we - wb + 63) / 64 * 16 : 0;  // iterations (16 per 64-row chunk)
+  uint4 va[VPL], vb[VPL];
+  if (T > 0) load_row(0, va);
+  for (int t = 0; t < T; t += 2) {
+    load_row(t + 1, vb);  // T is a multiple of 16: t + 1 < T
+    score_row(t & 15, va);
+    if (t + 2 < T) load_row(t + 2, va);
+    score_row((t + 1) & 15, vb);
+    if (((t + 2) & 15) == 0) {  // chunk done: offer its 64 rows
+      const int crow = wb + 64 * (t >> 4) + j * 4 + g;
+      // metadata filter: rows whose mask bit is clear are never offered
+      const bool ok = crow < we && (mask == nullptr || row_allowed(mask, crow));
 #pragma unroll
-    for (int qi = 0; qi < NQT; ++qi) L[qi].offer(cand[qi], crow, ok);
+      for (int qi = 0; qi < NQT; ++qi) L[qi].offer(cand[qi], crow, ok);
+    }
   }
 
   // block-level merge: the 4 wave lists of a query -> one list per block (4x fewer candidates
@@ -375,7 +388,7 @@ ValuPlan plan_scan_valu(int64_t nrows, int D, int dtype, int64_t nq, int k) {
   p.k_slot = valu_k_slot(k);
   p.nqt = nq <= 1 ? 1 : (nq <= 4 ? 4 : 8);
   p.q_slices = (int)((nq + p.nqt - 1) / p.nqt);
-  // Blocks: about kValuBlocks (2 per CU), so that every CU streams the same share of the store — a
+  // Blocks: about kValuBlocks (one per CU), so that every CU streams the same share of the store — a
   // count just above a multiple of the CU count leaves most CUs idle for the last round (config 2
   // had 391 blocks on 256 CUs).  Rows per wave: a multiple of 4 (one row per 16-lane group and
   // iteration), at least 16.

@@ -23,7 +23,7 @@ struct ValuPlan {
   int vpr, vpl, k_slot, nqt, q_slices, rows_per_wave, blocks, n_lists;
   bool ok;
 };
-constexpr int kValuBlocks = 512;  // target workgroups of a VALU scan (2 per CU of the 256)
+constexpr int kValuBlocks = 256;  // target workgroups of a VALU scan (one per CU; config-2 sweep)
 int valu_k_slot(int k);
 ValuPlan plan_scan_valu(int64_t nrows, int D, int dtype, int64_t nq, int k);
 // mask (every scan launcher): optional row mask, bit (r & 31) of word r >> 5 set = row r may be
