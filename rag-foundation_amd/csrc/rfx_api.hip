@@ -272,8 +272,13 @@ int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq,
               uint8_t* ws, hipStream_t st, const uint32_t* mask = nullptr) {
   if (ix.rows == 0 || nq == 0) return RFX_OK;
   if (L.kernel >= 1) {
-    void* qpad = ws + L.q_off;
-    rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, 2, qpad, st);
+    // the MFMA scans read queries as [nq_pad][dim]: a batch that is already a whole number of
+    // query groups (config 3: 256) is read in place, with no padding launch
+    const void* qpad = queries;
+    if (nq != L.mp.nq_pad || ((uintptr_t)queries & 15)) {
+      qpad = ws + L.q_off;
+      rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, 2, (void*)qpad, st);
+    }
     uint32_t* tau = (uint32_t*)(ws + L.tau_off);
     const int rc =
         L.kernel == 6 ? rfx::launch_scan_mfma6(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
