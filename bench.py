@@ -168,9 +168,9 @@ def main():
         if ev is not None:
             ev[1].record(stream)
         if world == 1:
-            return topk_merge(cs, cr, a.k, row_offset=r0, stream=stream, list_len=list_len)
+            return topk_merge(cs, cr, a.k, row_offset=r0, stream=stream, list_len=list_len, sorted=True)
         # rank-local top-k as all-gather records (global rows), one collective, one HIP merge
-        topk_merge_records(cs, cr, a.k, row_offset=r0, stream=stream, list_len=list_len, out=rec)
+        topk_merge_records(cs, cr, a.k, row_offset=r0, stream=stream, list_len=list_len, out=rec, sorted=True)
         return rdist.gather_merge_records(rec, a.k, comm=comm, stream=stream)
 
     for i in range(a.warmup):

@@ -161,6 +161,15 @@ int rfx_topk_merge_records(const float* cand_scores_d, const void* cand_rows_d, 
                            void* out_records_d, void* stream);
 int rfx_merge_gathered(const void* records_d, int world, int64_t nq, int k, float* out_scores_d,
                        int64_t* out_rows_d, void* stream);
+/* Merge of SORTED lists (rfx_scan_topk's output: each list of list_len entries best first, empty
+ * slots (-inf, INT32_MAX) at its tail): a list is read only while its entries can still be admitted,
+ * so the lists the admission bound rejects cost one load.  Writes [nq][k] scores + rows, or, when
+ * out_records_d is not NULL, [nq][k] records as rfx_topk_merge_records.  Replaces the same step
+ * as rfx_topk_merge_lists (the retrieval half of gemini_rag.py:517-551); unsorted input is an
+ * error of the caller (use rfx_topk_merge_lists). */
+int rfx_topk_merge_sorted(const float* cand_scores_d, const void* cand_rows_d, int rows_are_i64,
+                          int64_t nq, int64_t n_cand, int list_len, int k, int64_t row_offset,
+                          float* out_scores_d, int64_t* out_rows_d, void* out_records_d, void* stream);
 
 /* ---- RCCL communicators (SURVEY §8b rfx_init "RCCL comm if n>1", §8e) --------------------------
  * The all-gather of per-shard records runs on RCCL over xGMI from inside the library; the host

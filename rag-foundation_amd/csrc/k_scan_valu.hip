@@ -166,7 +166,7 @@ __device__ __forceinline__ float query_elem(const void* Q, int64_t i) {
     return f16_to_f32(((const uint16_t*)Q)[i]);
 }
 
-template <int K, bool R64, int NW, class Src>
+template <int K, bool R64, int NW, bool SORTED, class Src>
 __device__ __forceinline__ void merge_one(const Src& src, int64_t q, int list_len, int k_out, int64_t row_offset,
                                           float* __restrict__ out_s, int64_t* __restrict__ out_r,
                                           MergeRec* __restrict__ out_rec);
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
     if (!last) return;
     const AgentSrc src{cand_s, cand_r, (int64_t)n_lists * K};
     for (int qi = 0; qi < nqt; ++qi) {
-      merge_one<K, false, 4>(src, q0 + qi, K, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
+      merge_one<K, false, 4, true>(src, q0 + qi, K, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
       __syncthreads();
     }
     if (tid < nqt && tau) tau[q0 + tid] = 0u;  // every block's bound updates precede its arrival
@@ -552,7 +552,11 @@ __device__ __forceinline__ void rank_merge(const float (*ls)[K], const long long
 
 // One query's merge by a block of NW waves (the merge kernel: NW = 8; the fused single-launch
 // VALU search's last block: NW = 4).
-template <int K, bool R64, int NW, class Src>
+// SORTED: each list of list_len entries is sorted best first with its empty slots at the tail
+// (what every scan kernel writes, and the per-rank records of the multi-GPU path).  Then a list is
+// read only as far as its entries can still be admitted — the heads bound usually rejects a whole
+// list at its first entry — and the list-bound pass (every list's first k entries) is skipped.
+template <int K, bool R64, int NW, bool SORTED, class Src>
 __device__ __forceinline__ void merge_one(const Src& src, int64_t q, int list_len, int k_out, int64_t row_offset,
                                           float* __restrict__ out_s, int64_t* __restrict__ out_r,
                                           MergeRec* __restrict__ out_rec) {
@@ -598,7 +602,7 @@ __device__ __forceinline__ void merge_one(const Src& src, int64_t q, int list_le
     }
   }
   uint32_t m = 0u;  // list bound (below), reduced after the barrier
-  if (list_len > 1 && list_len >= k_out) {
+  if (!SORTED && list_len > 1 && list_len >= k_out) {
     for (int64_t j = tid; j < n / list_len; j += NT) {
       uint32_t mj = 0xffffffffu;  // min over the list's first k_out entries (sorted or not)
       for (int e0 = 0; e0 < k_out; e0 += 8) {  // 8 independent loads in flight per round
@@ -647,8 +651,27 @@ __device__ __forceinline__ void merge_one(const Src& src, int64_t q, int list_le
     const uint32_t u = tb & 0x80000000u ? tb & 0x7fffffffu : ~tb;  // inverse of ord_f32
     L.init_above(__uint_as_float(u), kNoRow);                      // admits score >= T
   }
-  for (int64_t base = (int64_t)w * 64; base < n; base += (int64_t)P * NW * 64)
-    merge_chunk<K, R64, P, NW>(src, q, base, n, lane, L);
+  if constexpr (SORTED) {
+    // lane walks list lb + lane while its entries still beat the wave list's admission bound
+    // (wave-uniform; it only rises): a sorted list's later entries cannot do better
+    const int64_t nl = n / list_len;
+    for (int64_t lb = (int64_t)w * 64; lb < nl; lb += NT) {
+      const int64_t li = lb + lane;
+      bool alive = li < nl;
+      for (int e = 0; e < list_len; ++e) {
+        float sc = -__builtin_inff();
+        long long rr = kNoRow;
+        if (alive) src.get(q, li * list_len + e, sc, rr);
+        const bool live = alive && rr >= 0 && rr != kNoRow && (R64 || rr != (long long)kEmptyRow);
+        L.offer(sc, rr, live);
+        alive = live && better64(sc, rr, L.ts, L.tr);
+        if (!__any(alive)) break;
+      }
+    }
+  } else {
+    for (int64_t base = (int64_t)w * 64; base < n; base += (int64_t)P * NW * 64)
+      merge_chunk<K, R64, P, NW>(src, q, base, n, lane, L);
+  }
   if (lane < K) {
     ls_lds[w][lane] = L.ls;
     lr_lds[w][lane] = L.lr;
@@ -670,32 +693,41 @@ __device__ __forceinline__ void merge_one(const Src& src, int64_t q, int list_le
   }
 }
 
-template <int K, bool R64, class Src>
+template <int K, bool R64, bool SORTED, class Src>
 __global__ __launch_bounds__(512) void merge_kernel(Src src, int list_len, int k_out, int64_t row_offset,
                                                     float* __restrict__ out_s, int64_t* __restrict__ out_r,
                                                     MergeRec* __restrict__ out_rec) {
-  merge_one<K, R64, 8>(src, (int64_t)blockIdx.x, list_len, k_out, row_offset, out_s, out_r, out_rec);
+  merge_one<K, R64, 8, SORTED>(src, (int64_t)blockIdx.x, list_len, k_out, row_offset, out_s, out_r, out_rec);
 }
 
 int launch_topk_merge_lists(const float* cs, const void* cr, int rows_are_i64, int64_t nq, int64_t n_cand,
                             int list_len, int k, int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec,
-                            hipStream_t st) {
+                            hipStream_t st, bool sorted) {
   const int kk = valu_k_slot(k);
   if (nq <= 0) return 0;
-  if (list_len < 1 || (list_len > 1 && n_cand % list_len != 0)) list_len = 1;
+  if (list_len < 1 || (list_len > 1 && n_cand % list_len != 0)) {
+    list_len = 1;
+    sorted = false;
+  }
   MergeRec* rec = (MergeRec*)out_rec;
+#define RFX_M2(KV, R, S)                                                                                  \
+  hipLaunchKernelGGL((merge_kernel<KV, R, S, FlatSrc<R>>), dim3((unsigned)nq), dim3(512), 0, st,          \
+                     FlatSrc<R>{cs, cr, n_cand}, list_len, k, row_offset, out_s, out_r, rec)
 #define RFX_M(KV)                                                                                     \
   if (kk == KV) {                                                                                     \
-    if (rows_are_i64)                                                                                 \
-      hipLaunchKernelGGL((merge_kernel<KV, true, FlatSrc<true>>), dim3((unsigned)nq), dim3(512), 0, st, \
-                         FlatSrc<true>{cs, cr, n_cand}, list_len, k, row_offset, out_s, out_r, rec);    \
+    if (rows_are_i64 && sorted)                                                                       \
+      RFX_M2(KV, true, true);                                                                         \
+    else if (rows_are_i64)                                                                            \
+      RFX_M2(KV, true, false);                                                                        \
+    else if (sorted)                                                                                  \
+      RFX_M2(KV, false, true);                                                                        \
     else                                                                                              \
-      hipLaunchKernelGGL((merge_kernel<KV, false, FlatSrc<false>>), dim3((unsigned)nq), dim3(512), 0,   \
-                         st, FlatSrc<false>{cs, cr, n_cand}, list_len, k, row_offset, out_s, out_r, rec); \
+      RFX_M2(KV, false, false);                                                                       \
     return 0;                                                                                         \
   }
   RFX_VALU_K_LIST(RFX_M)
 #undef RFX_M
+#undef RFX_M2
   return -1;
 }
 
@@ -711,8 +743,8 @@ int launch_merge_gathered(const void* rec, int world, int64_t nq, int k, float* 
   GatheredSrc src{(const MergeRec*)rec, nq, k, (int64_t)world * k};
 #define RFX_M(KV)                                                                                     \
   if (kk == KV) {                                                                                     \
-    hipLaunchKernelGGL((merge_kernel<KV, true, GatheredSrc>), dim3((unsigned)nq), dim3(512), 0, st, src, \
-                       k, k, 0, out_s, out_r, nullptr);                                               \
+    hipLaunchKernelGGL((merge_kernel<KV, true, true, GatheredSrc>), dim3((unsigned)nq), dim3(512), 0, st, \
+                       src, k, k, 0, out_s, out_r, nullptr);                                          \
     return 0;                                                                                         \
   }
   RFX_VALU_K_LIST(RFX_M)

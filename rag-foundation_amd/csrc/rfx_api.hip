@@ -778,6 +778,22 @@ int rfx_topk_merge_records(const float* cand_scores_d, const void* cand_rows_d, 
   return RFX_OK;
 }
 
+int rfx_topk_merge_sorted(const float* cand_scores_d, const void* cand_rows_d, int rows_are_i64, int64_t nq,
+                          int64_t n_cand, int list_len, int k, int64_t row_offset, float* out_scores_d,
+                          int64_t* out_rows_d, void* out_records_d, void* stream) {
+  if (k < 1 || k > 64) return fail(RFX_EINVAL, "k=%d out of range [1, 64]", k);
+  if (nq < 0 || n_cand < 0 || list_len < 1) return fail(RFX_EINVAL, "negative sizes / list_len < 1");
+  if (n_cand >= INT32_MAX) return fail(RFX_EINVAL, "n_cand must be < 2^31");
+  if (n_cand % list_len) return fail(RFX_EINVAL, "n_cand %% list_len != 0");
+  if (nq > 0 && !out_records_d && (!out_scores_d || !out_rows_d)) return fail(RFX_EINVAL, "null outputs");
+  if (rfx::launch_topk_merge_lists(cand_scores_d, cand_rows_d, rows_are_i64, nq, n_cand, list_len, k, row_offset,
+                                   out_records_d ? nullptr : out_scores_d, out_records_d ? nullptr : out_rows_d,
+                                   out_records_d, (hipStream_t)stream, /*sorted=*/true) != 0)
+    return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
 int rfx_merge_gathered(const void* records_d, int world, int64_t nq, int k, float* out_scores_d, int64_t* out_rows_d,
                        void* stream) {
   if (k < 1 || k > 64) return fail(RFX_EINVAL, "k=%d out of range [1, 64]", k);
@@ -878,7 +894,8 @@ int rfx_search_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k, c
   if (rc) return rc;
   // the scan's candidates are sorted lists: the merge bounds admission by the lists' k-th entries
   const int list_len = L.kernel ? L.mp.k_lane : L.vp.k_slot;
-  if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.n_cand, list_len, k, 0, out_scores_d, out_rows_d, nullptr, st) != 0)
+  if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.n_cand, list_len, k, 0, out_scores_d, out_rows_d, nullptr, st,
+                                   /*sorted=*/true) != 0)
     return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
   RFX_HIP(hipGetLastError());
   return RFX_OK;

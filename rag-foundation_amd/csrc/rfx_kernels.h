@@ -93,7 +93,8 @@ int launch_topk_merge(const float* cs, const void* cr, int rows_are_i64, int64_t
                       int k, int64_t row_offset, float* out_s, int64_t* out_r, hipStream_t st);
 int launch_topk_merge_lists(const float* cs, const void* cr, int rows_are_i64, int64_t nq, int64_t n_cand,
                             int list_len, int k, int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec,
-                            hipStream_t st);
+                            hipStream_t st,
+                            bool sorted = false);
 int launch_merge_gathered(const void* rec, int world, int64_t nq, int k, float* out_s, int64_t* out_r,
                           hipStream_t st);
 

@@ -141,6 +141,7 @@ SIGNATURES = {
     "rfx_topk_merge_lists": ([_p, _p, _i, _i64, _i64, _i, _i, _i64, _p, _p, _p], _i),
     "rfx_topk_merge_records": ([_p, _p, _i, _i64, _i64, _i, _i, _i64, _p, _p], _i),
     "rfx_merge_gathered": ([_p, _i, _i64, _i, _p, _p, _p], _i),
+    "rfx_topk_merge_sorted": ([_p, _p, _i, _i64, _i64, _i, _i, _i64, _p, _p, _p, _p], _i),
     "rfx_chunk_whitespace": ([_p, _i64, _i, _i, _p, _i64, _pi64], _i),
     "rfx_featurize": ([_p, _p, _i64, _i, _u64, _p, _p, _p, _i64, _pi64], _i),
     "rfx_embed_weights": ([_i, _i, _u64, _p, _p], _i),

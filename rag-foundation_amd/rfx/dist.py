@@ -156,7 +156,7 @@ class ShardedSearch:
 
         cs, cr = self.index.scan(queries, k, workspace=workspace, stream=stream)
         rec = topk_merge_records(cs, cr, k, row_offset=self.row_offset, stream=stream,
-                                 list_len=self.index.list_len(queries.shape[0], k))
+                                 list_len=self.index.list_len(queries.shape[0], k), sorted=True)
         return gather_merge_records(rec, k, self.comm, self.group, stream=stream)
 
 

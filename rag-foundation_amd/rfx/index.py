@@ -221,14 +221,21 @@ def _check_cands(cand_s: torch.Tensor, cand_r: torch.Tensor):
 
 
 def topk_merge(cand_s: torch.Tensor, cand_r: torch.Tensor, k: int, row_offset: int = 0, stream=None,
-               list_len: int = 1):
+               list_len: int = 1, sorted: bool = False):
     """Merge [nq][n_cand] candidates (rows int32 or int64) into the final top-k per query.
-    list_len: the candidates are sorted lists of that length (DeviceIndex.list_len); 1 = no hint."""
+    list_len: the candidates are lists of that length (DeviceIndex.list_len); 1 = no hint.
+    sorted: the lists are sorted best first with empty slots at the tail, as DeviceIndex.scan
+    writes them (rfx_topk_merge_sorted: a list is read only while it can still contribute)."""
     cand_s, cand_r = _check_cands(cand_s, cand_r)
     nq, ncand = cand_s.shape
     out_s = torch.empty((nq, k), dtype=torch.float32, device=cand_s.device)
     out_r = torch.empty((nq, k), dtype=torch.int64, device=cand_s.device)
     with torch.cuda.device(cand_s.device):
+        if sorted:
+            check(lib.rfx_topk_merge_sorted(ptr(cand_s), ptr(cand_r), int(cand_r.dtype == torch.int64), nq, ncand,
+                                            int(list_len), int(k), int(row_offset), ptr(out_s), ptr(out_r), None,
+                                            stream_ptr(stream)))
+            return out_s, out_r
         check(lib.rfx_topk_merge_lists(ptr(cand_s), ptr(cand_r), int(cand_r.dtype == torch.int64), nq, ncand,
                                        int(list_len), int(k), int(row_offset), ptr(out_s), ptr(out_r),
                                        stream_ptr(stream)))
@@ -236,7 +243,7 @@ def topk_merge(cand_s: torch.Tensor, cand_r: torch.Tensor, k: int, row_offset: i
 
 
 def topk_merge_records(cand_s: torch.Tensor, cand_r: torch.Tensor, k: int, row_offset: int = 0, stream=None,
-                       list_len: int = 1, out: torch.Tensor = None) -> torch.Tensor:
+                       list_len: int = 1, out: torch.Tensor = None, sorted: bool = False) -> torch.Tensor:
     """Merge as topk_merge, writing [nq][k][2] int64 records (score bits, global row): the
     all-gather input of the multi-GPU step (rfx.dist.pack's layout)."""
     cand_s, cand_r = _check_cands(cand_s, cand_r)
@@ -246,6 +253,11 @@ def topk_merge_records(cand_s: torch.Tensor, cand_r: torch.Tensor, k: int, row_o
     elif out.shape != (nq, k, 2) or out.dtype != torch.int64 or not out.is_contiguous():
         raise ValueError(f"out must be a contiguous int64 [{nq}][{k}][2] tensor")
     with torch.cuda.device(cand_s.device):
+        if sorted:
+            check(lib.rfx_topk_merge_sorted(ptr(cand_s), ptr(cand_r), int(cand_r.dtype == torch.int64), nq, ncand,
+                                            int(list_len), int(k), int(row_offset), None, None, ptr(out),
+                                            stream_ptr(stream)))
+            return out
         check(lib.rfx_topk_merge_records(ptr(cand_s), ptr(cand_r), int(cand_r.dtype == torch.int64), nq, ncand,
                                          int(list_len), int(k), int(row_offset), ptr(out), stream_ptr(stream)))
     return out

@@ -156,7 +156,8 @@ class ShardedIndex:
                     q = queries.to(torch.device("cuda", d), non_blocking=True)
                     m = row_mask[i] if row_mask is not None else None
                     cs, cr = sh.scan(q, k, stream=st, row_mask=m)
-                    rec = topk_merge_records(cs, cr, k, row_offset=base, stream=st, list_len=sh.list_len(nq, k))
+                    rec = topk_merge_records(cs, cr, k, row_offset=base, stream=st, list_len=sh.list_len(nq, k),
+                                             sorted=True)
             recs.append(rec)
         st0 = self._streams[0]
         if self.comm is not None:

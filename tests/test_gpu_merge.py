@@ -60,9 +60,9 @@ def test_merge_lists_matches_oracle(rindex, L, k, ties):
     cs = torch.from_numpy(s).cuda()
     for rows_dtype in (torch.int32, torch.int64):
         cr = torch.from_numpy(r).to(rows_dtype).cuda()
-        for ll in (L, 1):
-            out_s, out_r = rindex.topk_merge(cs, cr, k, list_len=ll)
-            assert np.array_equal(out_r.cpu().numpy(), ref_r), (ll, rows_dtype)
+        for ll, srt in ((L, False), (1, False), (L, True)):
+            out_s, out_r = rindex.topk_merge(cs, cr, k, list_len=ll, sorted=srt)
+            assert np.array_equal(out_r.cpu().numpy(), ref_r), (ll, rows_dtype, srt)
             assert np.array_equal(out_s.cpu().numpy(), ref_s)
 
 
@@ -147,12 +147,16 @@ def test_merge_few_queries_many_lists_matches_oracle(rindex, nq, n_lists, L, k, 
     s, r = sorted_lists(rng, nq, n_lists, L, 10_000_000, empty_frac=0.2, ties=ties)
     ref_s, ref_r = oracle_merge(s, r, k)
     for rows_dtype in (torch.int32, torch.int64):
-        for ll in (L, 1):
+        for ll, srt in ((L, False), (1, False), (L, True)):
             cs = torch.from_numpy(s.copy()).cuda()
             cr = torch.from_numpy(r).to(rows_dtype).cuda()
-            out_s, out_r = rindex.topk_merge(cs, cr, k, list_len=ll, row_offset=5)
-            assert np.array_equal(out_r.cpu().numpy(), np.where(ref_r >= 0, ref_r + 5, -1)), (ll, rows_dtype)
+            out_s, out_r = rindex.topk_merge(cs, cr, k, list_len=ll, row_offset=5, sorted=srt)
+            assert np.array_equal(out_r.cpu().numpy(), np.where(ref_r >= 0, ref_r + 5, -1)), (ll, rows_dtype, srt)
             assert np.array_equal(out_s.cpu().numpy(), ref_s)
+            if srt:  # the records form of the sorted merge carries the same rows and scores
+                rec = rindex.topk_merge_records(cs, cr, k, list_len=ll, row_offset=5, sorted=True)
+                rs, rr = rdist.unpack(rec)
+                assert torch.equal(rr, out_r) and torch.equal(rs, out_s)
 
 
 def test_merge_heads_bound_unsorted_and_all_empty(rindex):
@@ -165,3 +169,25 @@ def test_merge_heads_bound_unsorted_and_all_empty(rindex):
     cs, cr = torch.from_numpy(s.copy()).cuda(), torch.from_numpy(r).to(torch.int32).cuda()
     out_s, out_r = rindex.topk_merge(cs, cr, 10, list_len=16)  # wrong hint: unsorted lists
     assert np.array_equal(out_r.cpu().numpy(), ref_r) and np.array_equal(out_s.cpu().numpy(), ref_s)
+
+
+@pytest.mark.parametrize("dtype,nq", [("f32", 1), ("f32", 8), ("bf16", 1), ("bf16", 32), ("bf16", 100),
+                                      ("bf16", 256), ("f16", 200)])
+def test_sorted_merge_of_every_scan_plan(rindex, dtype, nq):
+    """Every scan kernel writes sorted lists: the sorted merge of its candidates equals the exact
+    (unsorted-safe) merge bit for bit, with tombstones and a row mask in play."""
+    ix = rindex.DeviceIndex(768, dtype)
+    ix.add_synthetic(21, 40_001)
+    ix.tombstone(list(range(0, 40_001, 97)))
+    q = rindex.synth_rows(22, 0, nq, 768, dtype)
+    words = np.full((40_001 + 31) // 32, -1, dtype=np.int32)
+    words[5:40] = 0
+    for m in (None, ix.mask_tensor(words)):
+        for k in (1, 10):
+            cs, cr = ix.scan(q, k, row_mask=m)
+            ll = ix.list_len(nq, k)
+            a_s, a_r = rindex.topk_merge(cs, cr, k, list_len=ll)
+            b_s, b_r = rindex.topk_merge(cs, cr, k, list_len=ll, sorted=True)
+            assert torch.equal(a_r, b_r) and torch.equal(a_s, b_s), (ix.plan(nq, k), m is None, k)
+            c_s, c_r = ix.search(q, k, row_mask=m)
+            assert torch.equal(c_r, a_r) and torch.equal(c_s, a_s)
