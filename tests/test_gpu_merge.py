@@ -155,7 +155,7 @@ def test_merge_few_queries_many_lists_matches_oracle(rindex, nq, n_lists, L, k, 
             assert np.array_equal(out_s.cpu().numpy(), ref_s)
             if srt:  # the records form of the sorted merge carries the same rows and scores
                 rec = rindex.topk_merge_records(cs, cr, k, list_len=ll, row_offset=5, sorted=True)
-                rs, rr = rdist.unpack(rec)
+                rs, rr = rdist.unpack(rec.unsqueeze(0))
                 assert torch.equal(rr, out_r) and torch.equal(rs, out_s)
 
 
