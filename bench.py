@@ -53,6 +53,8 @@ def parse():
     # oracle check of the last timed step (rank 0, N = 1): every `stride`-th query against
     # oracle.search.topk_blocks over ALL rows (read back after the timed region); 0 = off
     ap.add_argument("--oracle-stride", type=int, default=4)
+    ap.add_argument("--event-stride", type=int, default=1,
+                    help="bracket every Nth timed step with HIP events (kernel_ms = their average)")
     # rehearsal of the multi-GPU path on a one-GPU box: gloo transport, every rank on cuda:0,
     # and --check compares the sharded result with a whole-index search on rank 0
     ap.add_argument("--backend", default="rccl", choices=["rccl", "gloo"])
@@ -84,7 +86,8 @@ def cpu_model():
 
 
 KERNEL_NAMES = {0: "scan_valu_kernel", 1: "scan_mfma_kernel", 2: "scan_mfma2_kernel", 3: "scan_mfma3_kernel",
-                4: "scan_mfma4_kernel", 5: "scan_mfma5_kernel", 6: "scan_mfma6_kernel"}
+                4: "scan_mfma4_kernel", 5: "scan_mfma5_kernel", 6: "scan_mfma6_kernel",
+                7: "scan_mfma7_kernel", 8: "scan_mfma8_kernel"}
 
 
 def load_pmc_traffic(workload_key, kernel_name):
@@ -175,18 +178,19 @@ def main():
 
     for i in range(a.warmup):
         step(i)
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    ev_steps = list(range(0, a.steps, max(1, a.event_stride)))
+    evs = {i: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for i in ev_steps}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        out = step(i, evs[i])
+        out = step(i, evs.get(i))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    scan_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs) / a.steps
+    scan_ms = sum(e0.elapsed_time(e1) for e0, e1 in evs.values()) / len(evs)
     if world > 1:
         t = torch.tensor([elapsed, scan_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -230,13 +234,15 @@ def main():
                                 "host (gloo) rehearsal" if world > 1 else "none (one shard)"),
                    "scan_kernel": {0: "valu", 1: "mfma128", 2: "mfma256", 3: "mfma_qstationary128",
                                    4: "mfma_qstationary256", 5: "mfma_qstationary256_2wps",
-                                   6: "mfma16_qstationary256_2wps"}[kern]},
+                                   6: "mfma16_qstationary256_2wps", 7: "mfma16_qstationary128_2wps_xcdpair",
+                                   8: "mfma16_qstationary128_ksplit_pairs_xcdpair"}[kern]},
         "achieved_hbm_gbps_per_gpu": round(achieved, 1),
         "build_id": _lib.BUILD_ID,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": load_pmc_traffic(workload_key, kname),
                      "kernel": kname,
-                     "kernel_ms": round(scan_ms, 4), "alg_bytes_per_launch": alg_bytes},
+                     "kernel_ms": round(scan_ms, 4), "event_timed_launches": len(evs),
+                     "alg_bytes_per_launch": alg_bytes},
     }
 
     check_ok = True

@@ -1,0 +1,8 @@
+// k7_f16_1024.hip — instantiation unit of the d = 1024 scan kernel (k_scan_mfma7.h) for f16 rows.
+#include "k_scan_mfma7.h"
+
+namespace rfx {
+namespace k7 {
+RFX_K7_INSTANTIATE(RFX_F16, 1024, launch_f16_1024)
+}  // namespace k7
+}  // namespace rfx

@@ -126,7 +126,8 @@ __device__ __forceinline__ uint32_t tau_min(const uint8_t* p) {
 // some row of the tile reaches the bound; after such an update the list's best is published to
 // its slot (device atomicMax).
 // ROWMAP 0: value r of the lane is row rbase + (r & 3) + 8 (r >> 2) (32x32 accumulator layout);
-// ROWMAP 1: row rbase + (r & 7) + 16 (r >> 3) (the 16x16x32 pair-swapped layout of kernels 5, 6).
+// ROWMAP 1: row rbase + (r & 7) + 16 (r >> 3) (the 16x16x32 pair-swapped layout of kernels 5, 6);
+// ROWMAP 2: row rbase + (r & 3) + 16 (r >> 2) (four 16x16 row blocks of one query, kernel 7).
 // V: anything with float operator[](int) over 16 values (a 32x32 accumulator, or Acc4View).
 template <int KL, int ROWMAP = 0, class V = v4f32x16>
 __device__ __forceinline__ void fold(const V& acc, uint64_t* Ls, uint32_t& thr_o, int rbase, v4i32 tau_rsrc,
@@ -144,7 +145,9 @@ __device__ __forceinline__ void fold(const V& acc, uint64_t* Ls, uint32_t& thr_o
     for (int r = 0; r < 16; ++r) {
       const float s = acc[r];
       if (s >= thr) {  // NaN (tombstoned rows, rows past the end) never passes
-        const int row = ROWMAP == 0 ? rbase + (r & 3) + 8 * (r >> 2) : rbase + (r & 7) + 16 * (r >> 3);
+        const int row = ROWMAP == 0   ? rbase + (r & 3) + 8 * (r >> 2)
+                        : ROWMAP == 1 ? rbase + (r & 7) + 16 * (r >> 3)
+                                      : rbase + (r & 3) + 16 * (r >> 2);
         const uint64_t key = ((uint64_t)ord(s) << 32) | (uint32_t)(~(uint32_t)row);
         if (key > Ls[(KL - 1) * 64]) {
           int i = KL - 1;

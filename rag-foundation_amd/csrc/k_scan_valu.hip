@@ -144,6 +144,18 @@ struct AgentSrc {
   }
 };
 
+// One query's candidates staged in LDS by the fused search's last block (up to kFusedLdsCand).
+constexpr int kFusedLdsCand = 4096;
+struct LdsSrc {
+  const float* s;
+  const int* r;
+  int64_t n;
+  __device__ __forceinline__ void get(int64_t, int64_t i, float& sc, long long& rr) const {
+    sc = s[i];
+    rr = (long long)r[i];
+  }
+};
+
 // FUSED (the whole search in one launch, rfx_search on a VALU plan): the queries are read in the
 // index dtype and widened here (no widen kernel), and the last block of each query slice to finish
 // (agent-scope release/acquire on a per-slice counter) merges the slice's candidates into the final
@@ -334,10 +346,46 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
     }
     __syncthreads();
     if (!last) return;
-    const AgentSrc src{cand_s, cand_r, (int64_t)n_lists * K};
-    for (int qi = 0; qi < nqt; ++qi) {
-      merge_one<K, false, 4, true>(src, q0 + qi, K, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
-      __syncthreads();
+    const int64_t n = (int64_t)n_lists * K;
+    if (n <= kFusedLdsCand) {
+      // Bulk copy first: every candidate of the query is loaded with all loads in flight (one
+      // memory latency per 8 per thread) into LDS, then merged from there.  Merging straight from
+      // memory walks each sorted list with one dependent agent-scope load per entry.
+      __shared__ float bs[kFusedLdsCand];
+      __shared__ int br[kFusedLdsCand];
+      const LdsSrc lsrc{bs, br, n};
+      for (int qi = 0; qi < nqt; ++qi) {
+        const int64_t qo = (int64_t)(q0 + qi) * n;
+        for (int base = 0; base < (int)n; base += 256 * 8) {
+          uint32_t sv[8];
+          int rv[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int i = base + u * 256 + tid;
+            if (i < (int)n) {
+              sv[u] = __hip_atomic_load((const uint32_t*)cand_s + qo + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              rv[u] = __hip_atomic_load(cand_r + qo + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            const int i = base + u * 256 + tid;
+            if (i < (int)n) {
+              bs[i] = __uint_as_float(sv[u]);
+              br[i] = rv[u];
+            }
+          }
+        }
+        __syncthreads();
+        merge_one<K, false, 4, true>(lsrc, q0 + qi, K, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
+        __syncthreads();
+      }
+    } else {
+      const AgentSrc src{cand_s, cand_r, n};
+      for (int qi = 0; qi < nqt; ++qi) {
+        merge_one<K, false, 4, true>(src, q0 + qi, K, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
+        __syncthreads();
+      }
     }
     if (tid < nqt && tau) tau[q0 + tid] = 0u;  // every block's bound updates precede its arrival
     if (tid == 0) fo.ctr[blockIdx.y] = 0u;

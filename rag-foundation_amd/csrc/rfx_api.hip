@@ -154,7 +154,8 @@ int grow(Index& ix, int64_t need, hipStream_t st) {
 
 // ---- search workspace layout ------------------------------------------------------------------
 struct SearchLayout {
-  int kernel;        // 0 VALU (nq <= 8); 1 MFMA 128×BN (nq <= 64); 2 MFMA 256×256; 3 query-stationary MFMA
+  int kernel;        // 0 VALU (nq <= 8); 1 MFMA 128×BN (nq <= 64); 2 MFMA 256×256; 3 query-stationary MFMA;
+                     // 6 config-3 kernel (d 768); 7 / 8 d-1024 kernels (config 4)
   rfx::ValuPlan vp;
   rfx::MfmaPlan mp;
   int64_t n_cand;    // candidates per query
@@ -176,6 +177,27 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
       if (L.mp.ok) L.kernel = 6;
     }
     if (L.kernel == 0 && nq > 64) {
+      // d = 1024: kernel 8 (k-split wave pairs); the debug build's RFX_D1024_KERNEL=7 selects its
+      // predecessor kernel 7 (16 queries per wave) for A/B runs
+#ifdef RFX_DEBUG_BUILD
+      static const int d1024 = [] {
+        const char* e = getenv("RFX_D1024_KERNEL");
+        return e && *e ? atoi(e) : 8;
+      }();
+#else
+      constexpr int d1024 = 8;
+#endif
+      if (d1024 == 7) {
+#ifdef RFX_DEBUG_BUILD
+        L.mp = rfx::plan_scan_mfma7(ix.rows, ix.dim, ix.dtype, nq, k);
+        if (L.mp.ok) L.kernel = 7;
+#endif
+      } else {
+        L.mp = rfx::plan_scan_mfma8(ix.rows, ix.dim, ix.dtype, nq, k);
+        if (L.mp.ok) L.kernel = 8;
+      }
+    }
+    if (L.kernel == 0 && nq > 64) {
       L.mp = rfx::plan_scan_mfma3(ix.rows, ix.dim, ix.dtype, nq, k);
       if (L.mp.ok) L.kernel = 3;
     }
@@ -194,6 +216,12 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
     L.q_bytes = (size_t)L.mp.nq_pad * ix.dim * 2;
     if (L.kernel == 6)  // (the debug build's kernel-5 ablations use the same [nq_pad][16] table)
       tau_bytes = rfx::tau_bytes_mfma6(L.mp);
+#ifdef RFX_DEBUG_BUILD
+    else if (L.kernel == 7)
+      tau_bytes = rfx::tau_bytes_mfma7(L.mp);
+#endif
+    else if (L.kernel == 8)
+      tau_bytes = rfx::tau_bytes_mfma8(L.mp);
     else if (L.kernel >= 2)
       tau_bytes = (size_t)(L.mp.nq_pad + 256) * 4;  // + slack: 1 KB threshold DMA per group
   } else {
@@ -282,6 +310,10 @@ int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq,
     uint32_t* tau = (uint32_t*)(ws + L.tau_off);
     const int rc =
         L.kernel == 6 ? rfx::launch_scan_mfma6(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
+#ifdef RFX_DEBUG_BUILD
+        : L.kernel == 7 ? rfx::launch_scan_mfma7(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
+#endif
+        : L.kernel == 8 ? rfx::launch_scan_mfma8(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
         : L.kernel == 3 ? rfx::launch_scan_mfma3(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
         : L.kernel == 2 ? rfx::launch_scan_mfma2(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
                         : rfx::launch_scan_mfma(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, cs, cr, st, mask);

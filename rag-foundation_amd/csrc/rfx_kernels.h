@@ -85,6 +85,14 @@ int launch_scan_mfma6(const MfmaPlan& p, const void* X, int nrows, int D, int dt
                       uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
 int launch_scan_mfma6_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, int dtype, const void* Qpad, int nq,
                           uint32_t* tau, float* cs, int* cr, hipStream_t st);
+size_t tau_bytes_mfma7(const MfmaPlan& p);
+MfmaPlan plan_scan_mfma7(int64_t nrows, int D, int dtype, int64_t nq, int k);
+int launch_scan_mfma7(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
+size_t tau_bytes_mfma8(const MfmaPlan& p);
+MfmaPlan plan_scan_mfma8(int64_t nrows, int D, int dtype, int64_t nq, int k);
+int launch_scan_mfma8(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
 void launch_pad_queries(const void* Q, int64_t nq, int64_t nq_pad, int D, int esz, void* out,
                         hipStream_t st);
 

@@ -57,7 +57,8 @@ KERNEL_CASES = [
     (768, "bf16", 6, 5, 0),    # VALU, 8-query slices
     (768, "bf16", 40, 10, 1),  # 64-query MFMA tiles
     (768, "f16", 100, 16, 3),  # 128-query-stationary
-    (1024, "f16", 200, 10, 3),
+    (1024, "f16", 200, 10, 8),  # d-1024 kernel (config 4)
+    (1024, "f16", 200, 16, 3),
     (256, "bf16", 200, 10, 2),  # 256x256 tiles, other d
     (768, "bf16", 256, 10, 6),  # the config-3 kernel
     (768, "f16", 300, 4, 6),    # kernel 6, KL 4, two query groups
@@ -73,7 +74,16 @@ def test_masked_search_every_kernel(rindex, dim, dtype, nq, k, kern, density):
     check_masked(rindex, n, dim, dtype, nq, k, allowed, expect_kernel=kern)
 
 
-@pytest.mark.parametrize("dim,dtype,nq,k,kern", [KERNEL_CASES[0], KERNEL_CASES[2], KERNEL_CASES[6]])
+@pytest.mark.parametrize("n", [19_973, 65, 100])
+def test_masked_d1024_odd_mask_words(rindex, n):
+    """The d-1024 kernel's 64-row tiles span two mask words: the last tile's second word may lie past the
+    (rows + 31) / 32 words of the mask (n = 19,973: 625 words, 313 tiles)."""
+    allowed = np.random.default_rng(n).random(n) < 0.5
+    allowed[-1] = True
+    check_masked(rindex, n, 1024, "bf16", 256, 10, allowed, expect_kernel=8)
+
+
+@pytest.mark.parametrize("dim,dtype,nq,k,kern", [KERNEL_CASES[0], KERNEL_CASES[2], KERNEL_CASES[7]])
 def test_masked_search_ranges_and_tombstones(rindex, dim, dtype, nq, k, kern):
     # file-shaped masks (contiguous ranges, as LocalStore.row_mask builds them) plus tombstones
     n = 50_000

@@ -79,7 +79,7 @@ def test_cfg4_shard_fullsize(rindex):
     ix.add_synthetic(0, n, gen_row0=0)
     q = rindex.synth_rows(1, 0, nq, 1024, "f16")
     kern = ix.plan(nq, k)[0]
-    assert kern in (3, 6), kern
+    assert kern == 8, kern
     s, r = ix.search(q, k)
     torch.cuda.synchronize()
     oracle_check(ix, n, q, s, r, k)

@@ -194,9 +194,12 @@ def test_search_tombstones(rfx):
 # ---- search: MFMA path (batched bf16/f16) ----------------------------------------------------------
 def expected_mfma_kernel(nq, k, dim):
     """Mirror of make_layout (rfx_api.hip): 6 = 256-query-stationary, 2 waves/SIMD (d 768, k <= 10, nq > 128),
+    8 = 128-query-stationary k-split wave pairs, XCD-paired query groups (d 1024, k <= 10, nq > 64),
     3 = 128-query-stationary (d 768/1024, k <= 16, nq > 64), 2 = 256x256 tiles, 1 = 64-query tiles."""
     if nq > 128 and dim == 768 and k <= 10:
         return 6
+    if nq > 64 and dim == 1024 and k <= 10:
+        return 8
     if nq > 64 and dim in (768, 1024) and k <= 16:
         return 3
     if nq > 128:
@@ -298,7 +301,35 @@ def test_search_mfma4_many_duplicates(rfx):
 
 def test_search_mfma_dim1024(rfx):
     rindex, _ = rfx
-    run_search_check(rindex, 20000, 1024, "f16", 128, 10)
+    kern, _, _ = run_search_check(rindex, 20000, 1024, "f16", 128, 10)
+    assert kern == 8
+
+
+# ---- kernel 8 (d = 1024, config 4): 64-row tiles, k-split wave pairs, query groups paired on one XCD ----
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 127, 129, 8191, 16_385, 100_003])
+@pytest.mark.parametrize("dtype", ["bf16", "f16"])
+def test_search_d1024_ragged_rows(rfx, n, dtype):
+    """Ragged 64-row tails (NaN padding), fewer tiles than ranges (unpaired grid), paired grid."""
+    rindex, _ = rfx
+    kern, _, _ = run_search_check(rindex, n, 1024, dtype, 256, 10)
+    assert kern == 8
+
+
+@pytest.mark.parametrize("nq,k", [(65, 10), (128, 1), (129, 4), (200, 10), (256, 10), (300, 5), (512, 10)])
+def test_search_d1024_query_groups(rfx, nq, k):
+    """1..4 query groups of 128 (padded last group), lane lists of 4 and 10."""
+    rindex, _ = rfx
+    kern, _, _ = run_search_check(rindex, 60_000, 1024, "f16", nq, k)
+    assert kern == 8
+
+
+def test_search_d1024_ties_and_tombstones(rfx):
+    rindex, _ = rfx
+    rows64 = osynth.to_f64(osynth.synth_rows(7, 0, 30000, 1024, "f16"), "f16")
+    q64 = osynth.to_f64(osynth.synth_rows(8, 0, 1, 1024, "f16"), "f16")
+    top = int(osearch.topk(q64, rows64, 1)[1][0, 0])
+    kern, s, r = run_search_check(rindex, 30000, 1024, "f16", 256, 10, dup=(top, 3), tomb=[0, 7, 29999, top + 1])
+    assert kern == 8 and r[0, 0] == 3 and r[0, 1] == top
 
 
 def test_search_mfma_ties_and_tombstones(rfx):
