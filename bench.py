@@ -29,6 +29,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "top-k retrieval QPS + achieved HBM GB/s, 10M×768 k=10, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec; 6.29 TB/s measured float4 copy)
+F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 matrix (v_mfma_f32_16x16x4_f32)
 
 
 def parse():
@@ -87,7 +88,7 @@ def cpu_model():
 
 KERNEL_NAMES = {0: "scan_valu_kernel", 1: "scan_mfma_kernel", 2: "scan_mfma2_kernel", 3: "scan_mfma3_kernel",
                 4: "scan_mfma4_kernel", 5: "scan_mfma5_kernel", 6: "scan_mfma6_kernel",
-                7: "scan_mfma7_kernel", 8: "scan_mfma8_kernel"}
+                7: "scan_mfma7_kernel", 8: "scan_mfma8_kernel", 9: "scan_mfma9_kernel"}
 
 
 def load_pmc_traffic(workload_key, kernel_name):
@@ -235,7 +236,8 @@ def main():
                    "scan_kernel": {0: "valu", 1: "mfma128", 2: "mfma256", 3: "mfma_qstationary128",
                                    4: "mfma_qstationary256", 5: "mfma_qstationary256_2wps",
                                    6: "mfma16_qstationary256_2wps", 7: "mfma16_qstationary128_2wps_xcdpair",
-                                   8: "mfma16_qstationary128_ksplit_pairs_xcdpair"}[kern]},
+                                   8: "mfma16_qstationary128_ksplit_pairs_xcdpair",
+                                   9: "mfma_f32_qstationary128"}[kern]},
         "achieved_hbm_gbps_per_gpu": round(achieved, 1),
         "build_id": _lib.BUILD_ID,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -244,6 +246,11 @@ def main():
                      "kernel_ms": round(scan_ms, 4), "event_timed_launches": len(evs),
                      "alg_bytes_per_launch": alg_bytes},
     }
+    if kern == 9:  # f32 MFMA is 1/16 of the bf16 rate: this scan is matrix-core bound, not HBM bound
+        tflops = 2.0 * n_max * a.dim * a.nq / (scan_ms * 1e-3) / 1e12
+        result["roofline"].update({"bound": "mfma", "achieved": round(tflops, 2), "peak": F32_MFMA_PEAK_TFLOPS,
+                                   "unit": "TFLOP/s", "frac": round(tflops / F32_MFMA_PEAK_TFLOPS, 4),
+                                   "hbm_gbps": round(achieved, 1)})
 
     check_ok = True
     if rank == 0 and world == 1 and a.oracle_stride > 0:

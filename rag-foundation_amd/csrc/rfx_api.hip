@@ -155,7 +155,7 @@ int grow(Index& ix, int64_t need, hipStream_t st) {
 // ---- search workspace layout ------------------------------------------------------------------
 struct SearchLayout {
   int kernel;        // 0 VALU (nq <= 8); 1 MFMA 128×BN (nq <= 64); 2 MFMA 256×256; 3 query-stationary MFMA;
-                     // 6 config-3 kernel (d 768); 7 / 8 d-1024 kernels (config 4)
+                     // 6 config-3 kernel (d 768); 7 / 8 d-1024 kernels (config 4); 9 f32 stores
   rfx::ValuPlan vp;
   rfx::MfmaPlan mp;
   int64_t n_cand;    // candidates per query
@@ -201,6 +201,10 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
       L.mp = rfx::plan_scan_mfma3(ix.rows, ix.dim, ix.dtype, nq, k);
       if (L.mp.ok) L.kernel = 3;
     }
+    if (L.kernel == 0 && ix.dtype == RFX_F32) {
+      L.mp = rfx::plan_scan_mfma9(ix.rows, ix.dim, ix.dtype, nq, k);
+      if (L.mp.ok) L.kernel = 9;
+    }
     if (L.kernel == 0 && nq > 128) {
       L.mp = rfx::plan_scan_mfma2(ix.rows, ix.dim, ix.dtype, nq, k);
       if (L.mp.ok) L.kernel = 2;
@@ -213,7 +217,7 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
   size_t tau_bytes = 0;
   if (L.kernel) {
     L.n_cand = L.mp.n_lists * L.mp.k_lane;
-    L.q_bytes = (size_t)L.mp.nq_pad * ix.dim * 2;
+    L.q_bytes = (size_t)L.mp.nq_pad * ix.dim * (L.kernel == 9 ? 4 : 2);
     if (L.kernel == 6)  // (the debug build's kernel-5 ablations use the same [nq_pad][16] table)
       tau_bytes = rfx::tau_bytes_mfma6(L.mp);
 #ifdef RFX_DEBUG_BUILD
@@ -222,6 +226,8 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
 #endif
     else if (L.kernel == 8)
       tau_bytes = rfx::tau_bytes_mfma8(L.mp);
+    else if (L.kernel == 9)
+      tau_bytes = rfx::tau_bytes_mfma9(L.mp);
     else if (L.kernel >= 2)
       tau_bytes = (size_t)(L.mp.nq_pad + 256) * 4;  // + slack: 1 KB threshold DMA per group
   } else {
@@ -305,7 +311,7 @@ int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq,
     const void* qpad = queries;
     if (nq != L.mp.nq_pad || ((uintptr_t)queries & 15)) {
       qpad = ws + L.q_off;
-      rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, 2, (void*)qpad, st);
+      rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, L.kernel == 9 ? 4 : 2, (void*)qpad, st);
     }
     uint32_t* tau = (uint32_t*)(ws + L.tau_off);
     const int rc =
@@ -314,6 +320,7 @@ int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq,
         : L.kernel == 7 ? rfx::launch_scan_mfma7(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
 #endif
         : L.kernel == 8 ? rfx::launch_scan_mfma8(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
+        : L.kernel == 9 ? rfx::launch_scan_mfma9(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
         : L.kernel == 3 ? rfx::launch_scan_mfma3(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
         : L.kernel == 2 ? rfx::launch_scan_mfma2(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
                         : rfx::launch_scan_mfma(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, cs, cr, st, mask);

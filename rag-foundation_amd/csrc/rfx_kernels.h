@@ -93,6 +93,11 @@ size_t tau_bytes_mfma8(const MfmaPlan& p);
 MfmaPlan plan_scan_mfma8(int64_t nrows, int D, int dtype, int64_t nq, int k);
 int launch_scan_mfma8(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
                       uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
+// f32 stores (kernel 9): batched scan on v_mfma_f32_16x16x4_f32 for 16 < nq
+size_t tau_bytes_mfma9(const MfmaPlan& p);
+MfmaPlan plan_scan_mfma9(int64_t nrows, int D, int dtype, int64_t nq, int k);
+int launch_scan_mfma9(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
 void launch_pad_queries(const void* Q, int64_t nq, int64_t nq_pad, int D, int esz, void* out,
                         hipStream_t st);
 

@@ -53,11 +53,12 @@ class GpuRetriever:
     def __init__(self, registry=None, dim=None, dtype=None):
         self._registry = registry
         self.dim = int(os.environ.get("RFX_DIM", "768")) if dim is None else int(dim)
-        # bf16 stores by default: half the HBM bytes of f32 and the batched MFMA scans (kernels 1-6)
-        # serve micro-batches in one corpus pass; an f32 store's batches run the VALU scan in
-        # 8-query slices (one pass per slice).  Parity is defined on the stored values (the oracle
-        # widens stored rows exactly), so bf16 loses nothing against it; RFX_DTYPE=f32 keeps
-        # full-precision vectors where the application wants them.
+        # bf16 stores by default: half the HBM bytes of f32, and the bf16 MFMA scans run 8x the f32
+        # matrix rate.  An f32 store's micro-batches of more than 16 questions run kernel 9 (f32
+        # MFMA, one corpus pass per 128 queries); smaller ones the VALU scan in 8-query slices.
+        # Parity is defined on the stored values (the oracle widens stored rows exactly), so bf16
+        # loses nothing against it; RFX_DTYPE=f32 keeps full-precision vectors where the
+        # application wants them.
         self.dtype = os.environ.get("RFX_DTYPE", "bf16") if dtype is None else dtype
         # micro-batching of concurrent questions per store (RFX_BATCH=0 disables)
         self.batching = os.environ.get("RFX_BATCH", "1") != "0"

@@ -60,6 +60,7 @@ KERNEL_CASES = [
     (1024, "f16", 200, 10, 8),  # d-1024 kernel (config 4)
     (1024, "f16", 200, 16, 3),
     (256, "bf16", 200, 10, 2),  # 256x256 tiles, other d
+    (768, "f32", 100, 10, 9),   # f32 stores, batched (kernel 9)
     (768, "bf16", 256, 10, 6),  # the config-3 kernel
     (768, "f16", 300, 4, 6),    # kernel 6, KL 4, two query groups
 ]
@@ -83,7 +84,7 @@ def test_masked_d1024_odd_mask_words(rindex, n):
     check_masked(rindex, n, 1024, "bf16", 256, 10, allowed, expect_kernel=8)
 
 
-@pytest.mark.parametrize("dim,dtype,nq,k,kern", [KERNEL_CASES[0], KERNEL_CASES[2], KERNEL_CASES[7]])
+@pytest.mark.parametrize("dim,dtype,nq,k,kern", [KERNEL_CASES[0], KERNEL_CASES[2], KERNEL_CASES[7], KERNEL_CASES[8]])
 def test_masked_search_ranges_and_tombstones(rindex, dim, dtype, nq, k, kern):
     # file-shaped masks (contiguous ranges, as LocalStore.row_mask builds them) plus tombstones
     n = 50_000

@@ -33,6 +33,8 @@ def three_launch(rindex, ix, q, k, row_mask=None):
 def test_fused_equals_three_launches(rindex, dtype, nq, k):
     if dtype != "f32" and nq > 8:
         pytest.skip("bf16/f16 batches of > 8 queries take the MFMA plans")
+    if dtype == "f32" and nq > 16 and k <= 10:
+        pytest.skip("f32 batches of > 16 queries (k <= 10) take kernel 9")
     ix = rindex.DeviceIndex(768, dtype)
     ix.add_synthetic(5, 50_003)
     ix.tombstone([0, 17, 50_002])

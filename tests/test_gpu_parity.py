@@ -299,6 +299,48 @@ def test_search_mfma4_many_duplicates(rfx):
     assert float(s[0, 0]) == float(s[0, 9])
 
 
+# ---- kernel 9 (f32 stores, 16 < nq): f32 MFMA, 32 resident queries per wave, one wave per SIMD ------
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 8191, 30_001])
+def test_search_f32_batched_ragged_rows(rfx, n):
+    rindex, _ = rfx
+    kern, _, _ = run_search_check(rindex, n, 768, "f32", 256, 10)
+    assert kern == 9
+
+
+@pytest.mark.parametrize("nq,k", [(16, 10), (17, 10), (64, 4), (128, 1), (129, 10), (300, 5)])
+def test_search_f32_batched_query_groups(rfx, nq, k):
+    """nq <= 16 stays on the VALU slices; above, 1..3 query groups of 128, lane lists of 4 and 10."""
+    rindex, _ = rfx
+    kern, _, _ = run_search_check(rindex, 40_000, 768, "f32", nq, k)
+    assert kern == (9 if nq > 16 else 0)
+
+
+def test_search_f32_batched_ties_and_tombstones(rfx):
+    rindex, _ = rfx
+    rows64 = osynth.to_f64(osynth.synth_rows(7, 0, 20000, 768, "f32"), "f32")
+    q64 = osynth.to_f64(osynth.synth_rows(8, 0, 1, 768, "f32"), "f32")
+    top = int(osearch.topk(q64, rows64, 1)[1][0, 0])
+    kern, s, r = run_search_check(rindex, 20000, 768, "f32", 64, 10, dup=(top, 3), tomb=[0, 7, 19999, top + 1])
+    assert kern == 9 and r[0, 0] == 3 and r[0, 1] == top
+
+
+def test_f32_batched_matches_valu_slices(rfx):
+    """The same 64 queries through kernel 9 and through the VALU scan in 8-query slices."""
+    rindex, _ = rfx
+    ix = rindex.DeviceIndex(768, "f32")
+    ix.add_synthetic(21, 100_000)
+    q = rindex.synth_rows(22, 0, 64, 768, "f32")
+    s1, r1 = ix.search(q, 10)
+    assert ix.plan(64, 10)[0] == 9
+    parts = [ix.search(q[i:i + 8], 10) for i in range(0, 64, 8)]
+    s2 = torch.cat([p[0] for p in parts]).cpu().numpy()
+    r2 = torch.cat([p[1] for p in parts]).cpu().numpy()
+    s1, r1 = s1.cpu().numpy(), r1.cpu().numpy()
+    assert np.abs(s1 - s2).max() <= 2 * TOL
+    for qi, ki in zip(*np.nonzero(r1 != r2)):
+        assert abs(s1[qi, ki] - s2[qi, ki]) <= 2 * TIE
+
+
 def test_search_mfma_dim1024(rfx):
     rindex, _ = rfx
     kern, _, _ = run_search_check(rindex, 20000, 1024, "f16", 128, 10)
