@@ -41,6 +41,9 @@ int launch_scan_mfma6_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
     RFX_K6_DBG(32)
     RFX_K6_DBG(48)
     RFX_K6_DBG(41)
+    RFX_K6_DBG(64)
+    RFX_K6_DBG(256)
+    RFX_K6_DBG(320)
 
     default:
       return -1;

@@ -70,10 +70,60 @@ __device__ __forceinline__ void mask_rowmap1(V& a, uint32_t bits) {
     if (!((bits >> ((r & 7) + 16 * (r >> 3))) & 1u)) a[r >> 2][r & 3] = __builtin_nanf("");
 }
 
+// Debug-build ablations of the first tile's fold (MODE 64 / 256 below).  fold_nopub: the list insert
+// of mfc::fold (ROWMAP 1) without publishing the list's best to the slot table.  fold_first: the
+// lane's list is empty at tile 0, so each of the 16 values goes straight to its final position
+// rank = #{better values} (score desc, row asc; rows grow with r in ROWMAP 1), no shifting.
+template <int KL>
+__device__ __forceinline__ void fold_nopub(const Acc4View& acc, uint64_t* Ls, uint32_t& thr_o, int rbase) {
+  const float thr = thr_o ? unord(thr_o) : -__builtin_inff();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float s = acc[r];
+    if (s >= thr) {
+      const int row = rbase + (r & 7) + 16 * (r >> 3);
+      const uint64_t key = ((uint64_t)ord(s) << 32) | (uint32_t)(~(uint32_t)row);
+      if (key > Ls[(KL - 1) * 64]) {
+        int i = KL - 1;
+        for (; i > 0; --i) {
+          const uint64_t prev = Ls[(i - 1) * 64];
+          if (prev >= key) break;
+          Ls[i * 64] = prev;
+        }
+        Ls[i * 64] = key;
+      }
+    }
+  }
+  const uint32_t own = (uint32_t)(Ls[(KL - 1) * 64] >> 32);
+  thr_o = own > thr_o ? own : thr_o;
+}
+template <int KL, bool PUB>
+__device__ __forceinline__ void fold_first(const Acc4View& acc, uint64_t* Ls, uint32_t& thr_o, int rbase, v4i32 tau_rsrc,
+                                           uint32_t slot_voff) {
+  uint32_t best = 0u, kth = 0u;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const float si = acc[i];
+    int rank = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j != i) rank += (acc[j] > si) || (j < i && acc[j] == si);
+    if (si == si && rank < KL) {  // NaN never enters
+      const int row = rbase + (i & 7) + 16 * (i >> 3);
+      Ls[rank * 64] = ((uint64_t)ord(si) << 32) | (uint32_t)(~(uint32_t)row);
+      if (rank == 0) best = ord(si);
+      if (rank == KL - 1) kth = ord(si);
+    }
+  }
+  thr_o = kth > thr_o ? kth : thr_o;
+  if (PUB && best) batomic_umax(tau_rsrc, slot_voff, best);
+}
+
 // MODE: 0 production; kModeMask = row-masked variant (metadata filter); debug-build ablations:
 // 1 = no top-k epilogue (MFMAs kept live), 8 = no corpus stream after the prologue, 16 = corpus
 // DMA WITHOUT the non-temporal hint, 32 = every other k-step reuses the previous A fragments (half
-// the LDS reads; wrong scores, timing/energy only).
+// the LDS reads; wrong scores, timing/energy only), 64 = no slot-table publication at tile 0,
+// 256 = tile 0 folded by rank (fold_first).
 constexpr int kModeMask = 2097152;
 
 template <int DT, int KL, int D, int MODE = 0, int RING = kRing>
@@ -280,7 +330,18 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
       }
     if constexpr ((MODE & 1) == 0) {
       if constexpr ((MODE & kModeMask) != 0) mask_rowmap1(acc4, mask[tile] >> (8 * half));
-      fold<KL, 1>(Acc4View{acc4}, Ls, thr, tile * kTM + 8 * half, tau_rsrc, slot_voff, n_slow);
+      if constexpr ((MODE & (64 | 256)) != 0) {
+        if (it == 0) {
+          if constexpr ((MODE & 256) != 0)
+            fold_first<KL, (MODE & 64) == 0>(Acc4View{acc4}, Ls, thr, tile * kTM + 8 * half, tau_rsrc, slot_voff);
+          else
+            fold_nopub<KL>(Acc4View{acc4}, Ls, thr, tile * kTM + 8 * half);
+        } else {
+          fold<KL, 1>(Acc4View{acc4}, Ls, thr, tile * kTM + 8 * half, tau_rsrc, slot_voff, n_slow);
+        }
+      } else {
+        fold<KL, 1>(Acc4View{acc4}, Ls, thr, tile * kTM + 8 * half, tau_rsrc, slot_voff, n_slow);
+      }
     } else {
       if (acc4[0][0] == 12345.f && acc4[1][1] == 54321.f && acc4[2][2] == 1.f && acc4[3][3] == 2.f) Ls[0] = 1;
     }
