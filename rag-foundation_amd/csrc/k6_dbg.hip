@@ -44,6 +44,7 @@ int launch_scan_mfma6_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
     RFX_K6_DBG(64)
     RFX_K6_DBG(256)
     RFX_K6_DBG(320)
+    RFX_K6_DBG(512)
 
     default:
       return -1;

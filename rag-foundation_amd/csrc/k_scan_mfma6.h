@@ -123,7 +123,7 @@ __device__ __forceinline__ void fold_first(const Acc4View& acc, uint64_t* Ls, ui
 // 1 = no top-k epilogue (MFMAs kept live), 8 = no corpus stream after the prologue, 16 = corpus
 // DMA WITHOUT the non-temporal hint, 32 = every other k-step reuses the previous A fragments (half
 // the LDS reads; wrong scores, timing/energy only), 64 = no slot-table publication at tile 0,
-// 256 = tile 0 folded by rank (fold_first).
+// 256 = tile 0 folded by rank (fold_first), 512 = MFMAs of a k-step in snake order.
 constexpr int kModeMask = 2097152;
 
 template <int DT, int KL, int D, int MODE = 0, int RING = kRing>
@@ -311,9 +311,12 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-          for (int qb = 0; qb < 2; ++qb)
+          for (int qq = 0; qq < 2; ++qq) {
+            // MODE 512 (debug): snake order, consecutive MFMAs share an operand (A, B, A)
+            const int qb = (MODE & 512) != 0 ? (rb ? 1 - qq : qq) : qq;
             acc4[2 * rb + qb] = ks == 0 ? mfma16<DT>(cur.a[rb], bq[2 * ks + qb], v4f32x4{})
                                         : mfma16<DT>(cur.a[rb], bq[2 * ks + qb], acc4[2 * rb + qb]);
+          }
       }
     }
 
