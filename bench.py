@@ -30,6 +30,8 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "top-k retrieval QPS + achieved HBM GB/s, 10M×768 k=10, 1/2/4/8 MI355X"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md chip table (spec; 6.29 TB/s measured float4 copy)
 F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 matrix (v_mfma_f32_16x16x4_f32)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16/f16 MFMA (no sparsity)
+HBM_COPY_GBPS = 6290.0  # MI355X_MICROARCH.md: measured float4 copy
 
 
 def parse():
@@ -246,8 +248,15 @@ def main():
                      "kernel_ms": round(scan_ms, 4), "event_timed_launches": len(evs),
                      "alg_bytes_per_launch": alg_bytes},
     }
+    # MFMA utilisation alongside the HBM roofline (bf16/f16 dense peak), and the fraction
+    # of the measured copy bandwidth (MI355X_MICROARCH.md: 6.29 TB/s float4 copy)
+    flops = 2.0 * n_max * a.dim * a.nq
+    if kern in (1, 2, 3, 6, 7, 8):
+        result["roofline"]["mfma_tflops"] = round(flops / (scan_ms * 1e-3) / 1e12, 1)
+        result["roofline"]["mfma_frac_of_dense_peak"] = round(flops / (scan_ms * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4)
+    result["roofline"]["frac_of_measured_copy_bw"] = round(achieved / HBM_COPY_GBPS, 4)
     if kern == 9:  # f32 MFMA is 1/16 of the bf16 rate: this scan is matrix-core bound, not HBM bound
-        tflops = 2.0 * n_max * a.dim * a.nq / (scan_ms * 1e-3) / 1e12
+        tflops = flops / (scan_ms * 1e-3) / 1e12
         result["roofline"].update({"bound": "mfma", "achieved": round(tflops, 2), "peak": F32_MFMA_PEAK_TFLOPS,
                                    "unit": "TFLOP/s", "frac": round(tflops / F32_MFMA_PEAK_TFLOPS, 4),
                                    "hbm_gbps": round(achieved, 1)})
