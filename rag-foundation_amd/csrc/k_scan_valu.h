@@ -184,7 +184,9 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
       if (j == it) cand[qi] = acc;
     }
   };
-  const int T = we > wb ? (we - wb + 63) / 64 * 16 : 0;  // iterations (16 per 64-row chunk)
+  // iterations: 4 rows each, rounded up to the loop's unroll of 4 (not to a whole 64-row chunk: a
+  // wave's last chunk is usually partial, and iterations past its rows only re-read row wb)
+  const int T = we > wb ? (we - wb + 15) / 16 * 4 : 0;
   // three iterations in flight ahead of the one being scored (48 KB per wave at d 768 f32): one
   // wave per SIMD has nothing else to hide the loads' latency
   uint4 va[VPL], vb[VPL], vc[VPL], vd[VPL];
@@ -212,7 +214,7 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
   // Loads past the last iteration read row wb again (load_row clamps): unconditional, so no branch
   // around a load.
   for (int t = 0; t < T; t += 4) {
-    load_row(t + 3, vd);  // T is a multiple of 16: t + 3 < T
+    load_row(t + 3, vd);  // T is a multiple of 4: t + 3 < T
     score_row(t & 15, va);
     load_row(t + 4, va);
     score_row((t + 1) & 15, vb);
@@ -220,7 +222,8 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
     score_row((t + 2) & 15, vc);
     load_row(t + 6, vc);
     score_row((t + 3) & 15, vd);
-    if (((t + 4) & 15) == 0) {  // chunk done: offer its 64 rows
+    if (((t + 4) & 15) == 0 || t + 4 >= T) {  // chunk done (or the last, partial one): offer it
+      // lanes j of a partial chunk past its last iteration hold rows >= we: never offered
       const int crow = wb + 64 * (t >> 4) + j * 4 + g;
       // metadata filter: rows whose mask bit is clear are never offered
       const bool ok = crow < we && (mask == nullptr || row_allowed(mask, crow));
