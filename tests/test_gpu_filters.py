@@ -63,6 +63,8 @@ KERNEL_CASES = [
     (768, "f32", 100, 10, 9),   # f32 stores, batched (kernel 9)
     (768, "bf16", 256, 10, 6),  # the config-3 kernel
     (768, "f16", 300, 4, 6),    # kernel 6, KL 4, two query groups
+    (1024, "bf16", 256, 4, 8),  # kernel 8, KL 4
+    (768, "f32", 40, 3, 9),     # kernel 9, KL 4, one partial query group
 ]
 
 
