@@ -124,7 +124,23 @@ def main():
     from rfx import dist as rdist
     from rfx.index import DeviceIndex, synth_rows, topk_merge, topk_merge_records
 
-    comm = rdist.RcclComm.from_process_group(local) if world > 1 and a.backend == "rccl" else None
+    comm, exchange_note = None, None
+    if world > 1 and a.backend == "rccl":
+        # every rank must take the same exchange: agree on RCCL's init over the gloo control plane,
+        # and fall back to the host exchange (reported in the JSON line) rather than end the run
+        ok, err = 1, ""
+        try:
+            comm = rdist.RcclComm.from_process_group(local)
+        except Exception as e:  # noqa: BLE001 (any init failure: the fallback below is reported)
+            ok, err = 0, f"{type(e).__name__}: {e}"
+        flag = torch.tensor([ok], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if not int(flag[0]):
+            if comm is not None:
+                comm.close()
+            comm = None
+            exchange_note = f"RCCL communicator init failed on some rank ({err or 'see that rank'}); host (gloo) exchange"
+            print(exchange_note, file=sys.stderr, flush=True)
 
     dev = torch.device("cuda", local)
     r0, r1 = rdist.shard_range(a.rows, rank, world)
@@ -234,6 +250,7 @@ def main():
                    "rows": a.rows, "dim": a.dim, "nq": a.nq, "k": a.k, "parallelism": f"rowshard{world}",
                    "corpus_copies": copies, "launches_per_step": 1 if fused else 3,
                    "exchange": ("RCCL all-gather from librfx (rfx_allgather_records)" if comm is not None else
+                                exchange_note if exchange_note else
                                 "host (gloo) rehearsal" if world > 1 else "none (one shard)"),
                    "scan_kernel": {0: "valu", 1: "mfma128", 2: "mfma256", 3: "mfma_qstationary128",
                                    4: "mfma_qstationary256", 5: "mfma_qstationary256_2wps",
