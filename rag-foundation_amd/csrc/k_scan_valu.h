@@ -190,25 +190,44 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
   // three iterations in flight ahead of the one being scored (48 KB per wave at d 768 f32): one
   // wave per SIMD has nothing else to hide the loads' latency
   uint4 va[VPL], vb[VPL], vc[VPL], vd[VPL];
+  if constexpr (NQT == 1) {
+    // one query: each lane loads its own query elements straight into registers (every block
+    // reads the same d values: L2 hits), before the row loads, so waiting for them never waits
+    // for a row; clamped index + AND mask, no branch around a load.  No LDS, no barrier.
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) {
+      const int v = j + 16 * i;
+      const int vv = v < VPR ? v : VPR - 1;
+      const uint32_t m = v < VPR ? 0xffffffffu : 0u;
+      if constexpr (FUSED) {  // the query in the index dtype: the row's own 16-B layout
+        const uint4 u = *(const uint4*)((const uint8_t*)Qf + (int64_t)q0 * RB + (int64_t)vv * 16);
+#pragma unroll
+        for (int e = 0; e < EPV; ++e) qr[i * EPV + e] = __uint_as_float(__float_as_uint(elem<DT>(u, e)) & m);
+      } else {  // widened f32 queries: EPV floats per 16 B of row
+        const float* qf = (const float*)Qf + (int64_t)q0 * D + (int64_t)vv * EPV;
+#pragma unroll
+        for (int h = 0; h < EPV / 4; ++h) {
+          const uint4 u = *(const uint4*)(qf + 4 * h);
+          qr[i * EPV + 4 * h + 0] = __uint_as_float(u.x & m);
+          qr[i * EPV + 4 * h + 1] = __uint_as_float(u.y & m);
+          qr[i * EPV + 4 * h + 2] = __uint_as_float(u.z & m);
+          qr[i * EPV + 4 * h + 3] = __uint_as_float(u.w & m);
+        }
+      }
+    }
+  }
   if (T > 0) {  // the first rows are in flight while the query is staged
     load_row(0, va);
     load_row(1, vb);
     load_row(2, vc);
   }
-  for (int i = tid; i < NQT * D; i += 256) {
-    const int qi = i / D;
-    const int64_t src = (int64_t)(q0 + qi) * D + (i - qi * D);
-    q_lds[i] = qi >= nqt ? 0.f : FUSED ? query_elem<DT>(Qf, src) : ((const float*)Qf)[src];
-  }
-  __syncthreads();
-  if constexpr (NQT == 1) {
-#pragma unroll
-    for (int i = 0; i < VPL; ++i)
-#pragma unroll
-      for (int e = 0; e < EPV; ++e) {
-        const int v = j + 16 * i;
-        qr[i * EPV + e] = v < VPR ? q_lds[v * EPV + e] : 0.f;
-      }
+  if constexpr (NQT != 1) {
+    for (int i = tid; i < NQT * D; i += 256) {
+      const int qi = i / D;
+      const int64_t src = (int64_t)(q0 + qi) * D + (i - qi * D);
+      q_lds[i] = qi >= nqt ? 0.f : FUSED ? query_elem<DT>(Qf, src) : ((const float*)Qf)[src];
+    }
+    __syncthreads();
   }
 
   // Loads past the last iteration read row wb again (load_row clamps): unconditional, so no branch

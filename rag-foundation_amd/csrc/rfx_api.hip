@@ -920,7 +920,10 @@ int rfx_search_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k, c
   uint8_t* ws = (uint8_t*)ws_d;
   float* cs = (float*)(ws + L.cs_off);
   int32_t* cr = (int32_t*)(ws + L.cr_off);
-  if (L.kernel == 0 && ix->rows > 0 && nq > 0 && nq <= rfx::kValuFusedMaxNq && fused_enabled()) {
+  // (the one-launch kernel reads the caller's queries with 16-B loads: an unaligned buffer takes
+  // the three-launch path, whose widening copy is aligned)
+  if (L.kernel == 0 && ix->rows > 0 && nq > 0 && nq <= rfx::kValuFusedMaxNq && fused_enabled() &&
+      ((uintptr_t)queries_d & 15) == 0) {
     uint32_t* state = nullptr;
     if ((rc = fused_state(*ix, st, &state))) return rc;
     if (rfx::launch_search_valu_fused(L.vp, ix->data, (int)ix->rows, ix->dim, ix->dtype, queries_d, (int)nq, cs, cr,

@@ -94,3 +94,19 @@ def test_cfg2_shape_against_oracle(rindex):
     probs = osearch.check_topk(s.cpu().numpy(), r.cpu().numpy(), ref_s, ref_r,
                                lambda qi, rows: rows64[np.asarray(rows)] @ q64[qi], tol=1e-5, tie_band=2e-6)
     assert not probs, probs[:5]
+
+
+@pytest.mark.gpu
+def test_unaligned_queries_take_the_three_launch_path(rindex):
+    """The one-launch kernel reads queries with 16-B loads; a query buffer 4 B off alignment must
+    give the same answer (rfx_search routes it through the widening copy)."""
+    ix = rindex.DeviceIndex(768, "f32")
+    ix.add_synthetic(31, 20_000)
+    q = rindex.synth_rows(32, 0, 1, 768, "f32")
+    buf = torch.empty(768 + 1, dtype=torch.float32, device=q.device)
+    buf[1:].copy_(q[0])
+    qu = buf[1:].view(1, 768)
+    assert qu.data_ptr() % 16 == 4
+    s0, r0 = ix.search(q, 10)
+    s1, r1 = ix.search(qu, 10)
+    assert torch.equal(r0, r1) and torch.equal(s0, s1)
