@@ -40,7 +40,10 @@ constexpr int kQG = kPairs * kQW;         // 128 queries per workgroup
 constexpr int kSK = 128;                  // dims per stage
 constexpr int kRowB = kSK * 2;            // 256 B per row per stage
 constexpr int kSlot = kTM * kRowB;        // 16 KB: 64 rows × 128 dims
-constexpr int kRing = 5;                  // 5 slots, 4 stages (64 KB) in flight
+#ifndef RFX_K8_RING  // (a -DRFX_K8_RING=4 side build measures the ring-depth sensitivity)
+#define RFX_K8_RING 5
+#endif
+constexpr int kRing = RFX_K8_RING;        // 5 slots, 4 stages (64 KB) in flight
 constexpr int kGPW = 2;                   // LDS-DMA pieces per wave per stage (16 KB / 1 KB / 8 waves)
 constexpr int kTauW = 16;                 // u32 per query in the threshold table (KL <= 10 used)
 constexpr int kTauBytes = kQG * kTauW * 4;  // 8 KB: 8 DMA pieces, 1 per wave
