@@ -14,8 +14,8 @@
 // rows 32 kh .. 32 kh + 31), adds them, and runs kernel 6's epilogue on 32 rows × 32 queries.
 //   * Workgroup = 4 pairs × 32 queries = 128 queries; XCD-paired query groups, 64-row tiles,
 //     16-KB stages (64 rows × 128 dims, LDS image c ^ (r & 15)), default-cached corpus DMA: as
-//     kernel 7 (k_scan_mfma7.h), with a 5-slot ring (4 stages = 64 KB in flight) so that the
-//     32-KB partial-sum exchange fits beside it.
+//     kernel 7 (k_scan_mfma7.h), with a 4-slot ring (3 stages = 48 KB in flight; 5 slots measured
+//     2 % slower, 3 slots 4 % slower) beside the 32-KB partial-sum exchange.
 //   * Scores are a sum of two f32 partial dot products (each over 512 dims), within the parity
 //     tolerance of the f64 oracle like every other accumulation order.
 // Requires the index invariant of rfx_api.hip: rows [nrows, capacity) are NaN and capacity is a
@@ -40,10 +40,12 @@ constexpr int kQG = kPairs * kQW;         // 128 queries per workgroup
 constexpr int kSK = 128;                  // dims per stage
 constexpr int kRowB = kSK * 2;            // 256 B per row per stage
 constexpr int kSlot = kTM * kRowB;        // 16 KB: 64 rows × 128 dims
-#ifndef RFX_K8_RING  // (a -DRFX_K8_RING=4 side build measures the ring-depth sensitivity)
-#define RFX_K8_RING 5
+// Ring depth, measured by side builds (-DRFX_K8_RING=N, tools/gpu_k8ring.sh, config-4 shard):
+// 5 slots 7.17-7.20 ms, 4 slots 7.00-7.03 ms, 3 slots 7.45 ms per launch.
+#ifndef RFX_K8_RING
+#define RFX_K8_RING 4
 #endif
-constexpr int kRing = RFX_K8_RING;        // 5 slots, 4 stages (64 KB) in flight
+constexpr int kRing = RFX_K8_RING;        // 4 slots, 3 stages (48 KB) in flight
 constexpr int kGPW = 2;                   // LDS-DMA pieces per wave per stage (16 KB / 1 KB / 8 waves)
 constexpr int kTauW = 16;                 // u32 per query in the threshold table (KL <= 10 used)
 constexpr int kTauBytes = kQG * kTauW * 4;  // 8 KB: 8 DMA pieces, 1 per wave
@@ -172,11 +174,11 @@ __global__ __launch_bounds__(512, 1) void scan_mfma8_kernel(const uint16_t* __re
     return f;
   };
 
-  // Schedule: stage h's pieces go out during stage h - 4 (one per k-step of the wave) into the slot
-  // freed at stage h - 5's barrier; fragments are read one k-step ahead of their MFMAs; the stage-end
+  // Schedule: stage h's pieces go out during stage h - (kRing - 1) (one per k-step of the wave) into
+  // the slot freed at stage h - kRing's barrier; fragments are read one k-step ahead of their MFMAs; the stage-end
   // wait + barrier sit at the wave's last k-step of the stage.
   constexpr int AHEAD = kRing - 1;
-  constexpr int YNG = (kRing - 2) * kGPW;  // ops younger than the next stage (6)
+  constexpr int YNG = (kRing - 2) * kGPW;  // ops younger than the next stage (4)
   float* const xw = (float*)(lds + kXOff);  // exchange: [wave][16][64] f32
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
