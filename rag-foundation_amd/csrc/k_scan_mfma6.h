@@ -41,7 +41,10 @@ constexpr int kQG = kWaves * kQW;         // 256 queries per workgroup
 constexpr int kSK = 256;                  // dims per stage
 constexpr int kRowB = kSK * 2;            // 512 B per row per stage
 constexpr int kSlot = kTM * kRowB;        // 16 KB: 32 rows × 256 dims
-constexpr int kRing = 6;                  // default ring: 6 slots, 5 stages (80 KB) in flight
+#ifndef RFX_K6_RING  // (side builds with -DRFX_K6_RING=N measure the ring-depth sensitivity)
+#define RFX_K6_RING 6
+#endif
+constexpr int kRing = RFX_K6_RING;        // default ring: 6 slots, 5 stages (80 KB) in flight
 constexpr int kGPW = 2;                   // LDS-DMA pieces per wave per stage (16 KB / 1 KB / 8 waves)
 constexpr int kTauW = 16;                 // u32 per query in the threshold table (KL <= 10 used)
 constexpr int kTauBytes = kQG * kTauW * 4;  // 16 KB: 16 DMA pieces, 2 per wave
