@@ -20,7 +20,7 @@
 // cycles at a higher clock), with 2-row or 8-row × 128 B pieces alike.
 // Everything else as kernel 5: workgroup = 8 waves × 32 resident queries (192 VGPRs of B
 // fragments); 32-row tiles, block b takes tiles b, b + B, ...; a stage = 32 rows × 256 dims
-// (16 KB of rows) in a 6-slot ring, 5 stages in flight, one counted vmcnt + s_barrier per stage; per-lane
+// (16 KB of rows) in a 4-slot ring, 3 stages in flight, one counted vmcnt + s_barrier per stage; per-lane
 // sorted top-KL lists in LDS behind a pruning bound shared across workgroups through a per-query
 // slot table (k_mfma_common.h fold / tau_min).
 // Requires the index invariant of rfx_api.hip: rows [nrows, capacity) are NaN and capacity is a
@@ -41,10 +41,12 @@ constexpr int kQG = kWaves * kQW;         // 256 queries per workgroup
 constexpr int kSK = 256;                  // dims per stage
 constexpr int kRowB = kSK * 2;            // 512 B per row per stage
 constexpr int kSlot = kTM * kRowB;        // 16 KB: 32 rows × 256 dims
-#ifndef RFX_K6_RING  // (side builds with -DRFX_K6_RING=N measure the ring-depth sensitivity)
-#define RFX_K6_RING 6
+// Ring depth, measured by side builds (-DRFX_K6_RING=N, tools/gpu_k6ring.sh, alternating in one
+// call): config 3 6 slots 3.646 ms, 5 slots 3.614 ms, 4 slots 3.543-3.551 ms per launch.
+#ifndef RFX_K6_RING
+#define RFX_K6_RING 4
 #endif
-constexpr int kRing = RFX_K6_RING;        // default ring: 6 slots, 5 stages (80 KB) in flight
+constexpr int kRing = RFX_K6_RING;        // 4 slots, 3 stages (48 KB) in flight
 constexpr int kGPW = 2;                   // LDS-DMA pieces per wave per stage (16 KB / 1 KB / 8 waves)
 constexpr int kTauW = 16;                 // u32 per query in the threshold table (KL <= 10 used)
 constexpr int kTauBytes = kQG * kTauW * 4;  // 16 KB: 16 DMA pieces, 2 per wave
@@ -283,8 +285,8 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
         if constexpr ((MODE & 8) == 0)
           if (kk % (KPS / kGPW) == 0) issue_piece(g + RING - 1, (g + RING - 1) % RING, kk / (KPS / kGPW));
         if (kk == KB) {
-          // stage g+1 landed for this wave: ops younger than its pieces = stages g+2..g+5 (8)
-          // [+ a threshold refresh (2)]; lgkmcnt(0) + barrier: every wave has received its last
+          // stage g+1 landed for this wave: ops younger than its pieces = stages g+2..g+RING-1
+          // (YNG) [+ a threshold refresh (2)]; lgkmcnt(0) + barrier: every wave has received its last
           // fragment of slot g, which may be refilled from here on.
           if constexpr ((MODE & 8) == 0) {
             if (young(s))
