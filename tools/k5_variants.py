@@ -63,7 +63,7 @@ from rfx.index import topk_merge  # noqa: E402
 
 ref = None
 check = {}
-for m in [3] + [m for m in modes if m in (1000, 132072, 20000000, 20000070, 20000071, 20000064, 20000256, 20000320, 20000512)]:
+for m in [3] + [m for m in modes if m in (1000, 132072, 20000000, 20000070, 20000071, 20000064, 20000256, 20000320, 20000512, 20000016)]:
     launch(m)
     s, r = topk_merge(cs, cr, a.k, list_len=ix.list_len(a.nq, a.k))
     if ref is None:
