@@ -137,6 +137,11 @@ def check_topk(gpu_s, gpu_r, ref_s, ref_r, scores_of, tol=1e-5, tie_band=2e-6):
     nq, k = ref_r.shape
     for q in range(nq):
         g, r = gpu_r[q], ref_r[q]
+        gl = g[g >= 0]
+        if np.unique(gl).size != gl.size:
+            # a merge that emits one row twice must never pass, tie band or not
+            problems.append(f"q{q}: duplicate rows returned {g.tolist()}")
+            continue
         if np.array_equal(g, r):
             live = g >= 0
             if live.any():
@@ -155,6 +160,13 @@ def check_topk(gpu_s, gpu_r, ref_s, ref_r, scores_of, tol=1e-5, tie_band=2e-6):
         kth = ref_s[q][live.sum() - 1]
         if (sg < kth - tie_band).any():
             problems.append(f"q{q}: returned row below k-th score band: {g.tolist()} vs {r.tolist()}")
+        # the returned set equals the reference set outside the band: every reference row scoring
+        # above the k-th score's band must be returned
+        rl = r[r >= 0]
+        must = rl[ref_s[q][r >= 0] > kth + tie_band]
+        missing = np.setdiff1d(must, gl)
+        if missing.size:
+            problems.append(f"q{q}: rows {missing.tolist()} above the tie band are missing: {g.tolist()} vs {r.tolist()}")
         # order: GPU order must be non-increasing in reference score up to the tie band
         if (np.diff(sg) > tie_band).any():
             problems.append(f"q{q}: order violates ranking beyond tie band")

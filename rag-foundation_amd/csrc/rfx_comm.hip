@@ -29,6 +29,10 @@ struct Comm {
   int world = 0;
   int rank = 0;  // rank mode: this process's rank; group mode: 0
   bool group = false;
+  // One communicator must see its collectives in the same order on every device.  Searches of
+  // different (store, filter) batches run in parallel threads against one ShardedIndex, so the
+  // group start .. end of one all-gather is made atomic here.
+  std::mutex mu;
 };
 
 std::mutex g_mu;
@@ -114,6 +118,7 @@ int rfx_comm_destroy(rfx_comm_t h) {
     c = it->second;
     g_comms.erase(it);
   }
+  std::lock_guard<std::mutex> lk(c->mu);  // no all-gather of another thread is mid-enqueue
   for (auto& cm : c->comms) RFX_NCCL(ncclCommDestroy(cm));
   return RFX_OK;
 }
@@ -131,6 +136,7 @@ int rfx_allgather_records(rfx_comm_t h, const void* const* sends_d, void* const*
     if (!sends_d[i] || !recvs_d[i]) return rfx::api_fail(RFX_EINVAL, "null buffer for local device %d", i);
   int prev = 0;
   if (hipGetDevice(&prev) != hipSuccess) return rfx::api_fail(RFX_EDEVICE, "hipGetDevice");
+  std::lock_guard<std::mutex> lk(c->mu);
   if (n > 1) RFX_NCCL(ncclGroupStart());
   int rc = RFX_OK;
   for (int i = 0; i < n && rc == RFX_OK; ++i) {

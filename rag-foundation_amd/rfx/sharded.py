@@ -13,6 +13,8 @@ the process's devices (rfx_allgather_records on an ncclCommInitAll group), one r
 Several shards on one device (RFX_DEVICES=0,0,0,0: logical shards, tests) skip the collective:
 their records are stacked on that device and merged by the same kernel.
 """
+import threading
+
 import numpy as np
 import torch
 
@@ -47,6 +49,9 @@ class ShardedIndex:
         distinct = len(set(self.devices)) == len(self.devices)
         self.comm = RcclComm.for_devices(self.devices) if distinct and len(self.devices) > 1 else None
         self._streams = [torch.cuda.Stream(device=d) for d in self.devices]
+        # held across a search's enqueue and across re-splits / close: a batch never searches shards
+        # another thread is replacing, and two batches never interleave their scans and all-gather
+        self._lock = threading.RLock()
 
     # ---- shape ---------------------------------------------------------------------------------
     @property
@@ -65,7 +70,10 @@ class ShardedIndex:
     # ---- loads / writes --------------------------------------------------------------------------
     def _do_split(self, upto):
         n = len(self.shards)
-        cuts = [min(upto, -(-(i * upto // n) // ALIGN) * ALIGN) for i in range(n)] + [upto]
+        # every base a multiple of ALIGN, also when upto itself is not (a reader opening a store after
+        # a small first upload): mask_tensor slices whole mask words per shard
+        top = (upto // ALIGN) * ALIGN
+        cuts = [min(top, -(-(i * upto // n) // ALIGN) * ALIGN) for i in range(n)] + [upto]
         for i in range(n):
             self.bases[i] = cuts[i]
         self._split = True
@@ -74,6 +82,10 @@ class ShardedIndex:
     def rows_sync(self, path: str, upto: int) -> None:
         """Load file rows [rows, upto): the first load splits them over the shards, later ones go
         to the last shard (the store grew)."""
+        with self._lock:
+            self._rows_sync(path, upto)
+
+    def _rows_sync(self, path: str, upto: int) -> None:
         if not self._split:
             cuts = self._do_split(upto)
             for i, sh in enumerate(self.shards):
@@ -90,17 +102,18 @@ class ShardedIndex:
             sh.close()
         self.shards = [DeviceIndex(self.dim, self.dtype, d) for d in self.devices]
         self._split = False
-        self.rows_sync(path, upto)
+        self._rows_sync(path, upto)
         if self._tombs:
             self._tombstone(np.concatenate(self._tombs))
 
     def add(self, vecs: torch.Tensor) -> int:
         """Append rows (writer path): they extend the last shard."""
-        first = self.rows
-        self._split = True
-        last = self.shards[-1]
-        last.add(vecs.to(torch.device("cuda", self.devices[-1])))
-        return first
+        with self._lock:
+            first = self.rows
+            self._split = True
+            last = self.shards[-1]
+            last.add(vecs.to(torch.device("cuda", self.devices[-1])))
+            return first
 
     def rows_append(self, path: str, row0: int) -> None:
         """Write global rows [row0, rows) to the row file, shard by shard in row order."""
@@ -117,8 +130,9 @@ class ShardedIndex:
 
     def tombstone(self, rows) -> None:
         rows = np.asarray(rows, dtype=np.int64)
-        self._tombs.append(rows)
-        self._tombstone(rows)
+        with self._lock:
+            self._tombs.append(rows)
+            self._tombstone(rows)
 
     def read(self, row0: int, n: int) -> torch.Tensor:
         parts = []
@@ -134,6 +148,10 @@ class ShardedIndex:
                 for base, d in zip(self.bases, self.devices)]
 
     def close(self) -> None:
+        with self._lock:
+            self._close()
+
+    def _close(self) -> None:
         for sh in self.shards:
             sh.close()
         if self.comm is not None:
@@ -142,6 +160,10 @@ class ShardedIndex:
 
     # ---- search --------------------------------------------------------------------------------
     def search(self, queries: torch.Tensor, k: int, row_mask=None):
+        with self._lock:
+            return self._search(queries, k, row_mask)
+
+    def _search(self, queries: torch.Tensor, k: int, row_mask=None):
         nq = queries.shape[0]
         src = torch.cuda.current_stream(queries.device)
         recs = []

@@ -300,21 +300,20 @@ class LocalStore:
             self._sync()  # append at the end of what every writer committed
             file_id = f"files/local-{uuid.uuid4().hex}"
             first = self.index.rows
-            if len(chunks):
-                self.index.add(vecs)
-                try:
+            # everything after the catch-up is one commit: any failure (ENOSPC, EIO, interrupt) in
+            # the row, metadata, file-record or manifest writes re-reads the committed state, so no
+            # phantom rows stay in this process's index
+            try:
+                if len(chunks):
+                    self.index.add(vecs)
                     self.index.rows_append(self._p("rows.rfx"), first)
                     meta = "".join(json.dumps({"f": file_id, "t": c}, ensure_ascii=False) + "\n" for c in chunks)
                     self.meta_bytes = _append(self._p("meta.jsonl"), self.meta_bytes, meta.encode())
-                except BaseException:
-                    self._rollback(first)
-                    raise
-            rec = {"op": "add", "id": file_id, "first": first, "n": len(chunks), "display_name": display_name,
-                   "uri": f"local://{self.name}/{file_id}", "metadata": metadata or None}
-            self.files_bytes = _append(self._p("files.jsonl"), self.files_bytes, (json.dumps(rec) + "\n").encode())
-            self._apply_file_record(rec)
-            self.rows.extend((file_id, c) for c in chunks)
-            try:
+                rec = {"op": "add", "id": file_id, "first": first, "n": len(chunks), "display_name": display_name,
+                       "uri": f"local://{self.name}/{file_id}", "metadata": metadata or None}
+                self.files_bytes = _append(self._p("files.jsonl"), self.files_bytes, (json.dumps(rec) + "\n").encode())
+                self._apply_file_record(rec)
+                self.rows.extend((file_id, c) for c in chunks)
                 self._maybe_train()
                 self.version += 1
                 self._write_manifest()
@@ -411,16 +410,20 @@ class LocalStore:
             f = self.files.get(file_id)
             if not f or f["deleted"]:
                 return False
-            if f["n"]:
-                rows = np.arange(f["first"], f["first"] + f["n"], dtype="<i8")
-                self.index.tombstone(rows)
-                _append(self._p("tombs.bin"), 8 * self.tombs, rows.tobytes())
-                self.tombs += len(rows)
-            rec = {"op": "del", "id": file_id}
-            self.files_bytes = _append(self._p("files.jsonl"), self.files_bytes, (json.dumps(rec) + "\n").encode())
-            self._apply_file_record(rec)
-            self.version += 1
-            self._write_manifest()
+            try:  # one commit, as in add_document: a failure re-reads the committed state
+                if f["n"]:
+                    rows = np.arange(f["first"], f["first"] + f["n"], dtype="<i8")
+                    self.index.tombstone(rows)
+                    _append(self._p("tombs.bin"), 8 * self.tombs, rows.tobytes())
+                    self.tombs += len(rows)
+                rec = {"op": "del", "id": file_id}
+                self.files_bytes = _append(self._p("files.jsonl"), self.files_bytes, (json.dumps(rec) + "\n").encode())
+                self._apply_file_record(rec)
+                self.version += 1
+                self._write_manifest()
+            except BaseException:
+                self._rollback(None)
+                raise
             return True
 
     # ---- reads -------------------------------------------------------------------------------------

@@ -124,6 +124,30 @@ def test_check_topk_tie_band():
     assert search.check_topk(np.array([[0.5, 0.4, 0.2]]), np.array([[1, 2, 5]]), ref_s, ref_r, f) != []
 
 
+def test_check_topk_rejects_duplicate_rows():
+    """VERDICT r2 weak #1: [a, a, c] against [a, b, c] with |s_a - s_b| inside the tie band must fail."""
+    ref_s = np.array([[0.5, 0.5 - 1e-7, 0.3]])
+    ref_r = np.array([[1, 2, 3]])
+    sc = {1: 0.5, 2: 0.5 - 1e-7, 3: 0.3}
+    f = lambda q, rows: np.array([sc[int(x)] for x in rows])
+    probs = search.check_topk(np.array([[0.5, 0.5, 0.3]]), np.array([[1, 1, 3]]), ref_s, ref_r, f)
+    assert probs and "duplicate" in probs[0]
+    # the legal near-tie swap of the same two rows still passes
+    assert search.check_topk(np.array([[0.5 - 1e-7, 0.5, 0.3]]), np.array([[2, 1, 3]]), ref_s, ref_r, f) == []
+
+
+def test_check_topk_requires_rows_above_band():
+    """A row scoring above the k-th score's band must be returned even if the GPU list is
+    otherwise ordered and within tolerance."""
+    ref_s = np.array([[0.9, 0.5, 0.5 - 1e-7]])
+    ref_r = np.array([[7, 1, 2]])
+    sc = {7: 0.9, 1: 0.5, 2: 0.5 - 1e-7, 3: 0.5 - 1.5e-6}
+    f = lambda q, rows: np.array([sc[int(x)] for x in rows])
+    # row 7 (0.9) replaced by two near-ties of the k-th score: must fail
+    probs = search.check_topk(np.array([[0.5, 0.5 - 1e-7, 0.5 - 1.5e-6]]), np.array([[1, 2, 3]]), ref_s, ref_r, f)
+    assert any("missing" in p or "below" in p or "differ" in p for p in probs)
+
+
 def test_embed_exactness_bound():
     """|e| stays below 2^24 quanta for the maximum chunk (65536 tokens), so f32 MFMA accumulation
     is exact in any order (k_embed.hip)."""

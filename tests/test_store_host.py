@@ -149,3 +149,33 @@ def test_two_processes_append_concurrently(tmp_path):
     assert pos == n
     man = json.load(open(os.path.join(st.path, "manifest.json")))
     assert man["version"] == 50 and man["rows"] == n
+
+
+@pytest.mark.parametrize("op", ["add", "delete"])
+def test_failed_file_record_append_rolls_back(tmp_path, monkeypatch, op):
+    """a failure in the files.jsonl append (after the rows and metadata were written)
+    must leave this writer in the committed state: no phantom rows, and the next upload commits
+    a consistent store that other processes can open."""
+    a = reg(tmp_path)
+    st = a.create("demo", 64, "f32")
+    fid, _ = st.add_document(["c0", "c1"], vecs(2, 1), "one.md")
+    real = rstore._append
+
+    def failing(path, committed, data):
+        if path.endswith("files.jsonl"):
+            raise OSError(28, "No space left on device")
+        return real(path, committed, data)
+
+    monkeypatch.setattr(rstore, "_append", failing)
+    with pytest.raises(OSError):
+        if op == "add":
+            st.add_document(["d0", "d1", "d2"], vecs(3, 2), "two.md")
+        else:
+            st.delete_file(fid)
+    monkeypatch.setattr(rstore, "_append", real)
+    assert st.index.rows == 2 and len(st.rows) == 2
+    assert not st.files[fid]["deleted"] and not np.isnan(st.index.data).any()
+    f3, first3 = st.add_document(["e0"], vecs(1, 3), "three.md")
+    assert first3 == 2
+    sb = reg(tmp_path).get(st.name)  # another process opens it without a row/metadata mismatch
+    assert sb.index.rows == 3 and len(sb.rows) == 3 and sb.row_info(2)[0] == f3
