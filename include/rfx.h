@@ -171,6 +171,36 @@ int rfx_topk_merge_sorted(const float* cand_scores_d, const void* cand_rows_d, i
                           int64_t nq, int64_t n_cand, int list_len, int k, int64_t row_offset,
                           float* out_scores_d, int64_t* out_rows_d, void* out_records_d, void* stream);
 
+/* ---- exact two-pass scan over an int8 copy of the store ------------------------
+ * The int8 representation of SURVEY §8a row a3 / §8b (dtype I8), kept BESIDE the bf16/f16 rows so
+ * that results stay exact: the same top-k as rfx_search on the rows alone (gemini_rag.py:517-551).
+ * rfx_index_screen(h, 1) builds the copy (per 32-row tile: scale amax/127, codes rint(x/scale),
+ * a live-row word; + the max row norm and max quantisation-error norm) and keeps it current
+ * through add / add_synthetic / rows_sync / tombstone.  Then batched searches (64 < nq, k <= 10,
+ * dim 768 or 1024, bf16/f16; the plans of kernels 6 and 8) run: an int8 MFMA screen that keeps
+ * every row whose exact score can still reach the query's k-th best (a rigorous Cauchy-Schwarz
+ * bound of the quantisation error), an exact re-score of those rows from the stored rows, and —
+ * gated on the device, only when a query's survivors may be incomplete — the exact scan for the
+ * batch.  mode 0 drops the copy; mode 2 = on, with every batch sent to the exact fallback (tests).
+ * Costs dim bytes per row of extra HBM.  EUNSUPPORTED for f32 stores and other dims. */
+int rfx_index_screen(rfx_index_t h, int mode, void* stream);
+/* Inspection (tests): tiles [tile0, tile0 + ntiles) of the copy to host buffers (any may be NULL):
+ * codes [ntiles*32][dim] int8, scales [ntiles] f32, live words [ntiles], stats [2] f32. */
+int rfx_index_screen_read(rfx_index_t h, int64_t tile0, int64_t ntiles, int8_t* codes_h, float* scales_h,
+                          uint32_t* live_h, float* stats_h);
+/* The kernel rfx_search runs for (nq, k): 0 VALU, 1/2/3/6/8/9 exact MFMA scans, 10 the two-pass scan. */
+int rfx_search_plan(rfx_index_t h, int64_t nq, int k, int* out_kernel);
+/* After a two-pass search with workspace ws_d (stream-ordered; this call synchronises): per query
+ * {kept screen candidates, survivors re-scored (-1 = sent to the fallback)} into diag_h [nq][2], and
+ * whether the exact fallback ran for the batch (*fallback_h != 0). */
+int rfx_screen_diag(rfx_index_t h, int64_t nq, int k, const void* ws_d, int32_t* diag_h, uint32_t* fallback_h);
+/* rfx_search_masked writing [nq][k] merge records {f32 score, i32 pad, i64 row + row_offset} (the
+ * all-gather input of the multi-GPU step) instead of scores and rows: one call per shard, whatever
+ * kernel the plan picks (an empty shard writes padding records). */
+int rfx_search_records(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d,
+                       int64_t mask_words, int64_t row_offset, void* out_records_d, void* ws_d, size_t ws_bytes,
+                       void* stream);
+
 /* ---- RCCL communicators (SURVEY §8b rfx_init "RCCL comm if n>1", §8e) --------------------------
  * The all-gather of per-shard records runs on RCCL over xGMI from inside the library; the host
  * language only bootstraps the communicator (passes the 128-byte id from rank 0 to the others).

@@ -16,10 +16,10 @@ int launch_scan_mfma6_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
     const uint16_t* Qh = (const uint16_t*)Qpad;
     if (mode == 70)
       hipLaunchKernelGGL((k6::scan_mfma6_kernel<RFX_BF16, 4, 768, 0, 6>), dim3(p.blocks, p.q_blocks), dim3(512), 0, st,
-                         Xh, Qh, nq, ntiles, tau, cs, cr, p.n_lists, nullptr);
+                         Xh, Qh, nq, ntiles, tau, cs, cr, p.n_lists, nullptr, nullptr);
     else
       hipLaunchKernelGGL((k6::scan_mfma6_kernel<RFX_BF16, 4, 768, 0, 7>), dim3(p.blocks, p.q_blocks), dim3(512), 0, st,
-                         Xh, Qh, nq, ntiles, tau, cs, cr, p.n_lists, nullptr);
+                         Xh, Qh, nq, ntiles, tau, cs, cr, p.n_lists, nullptr, nullptr);
     return 0;
   }
   if (p.k_lane != 10) return -1;
@@ -31,7 +31,7 @@ int launch_scan_mfma6_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
 #define RFX_K6_DBG(M)                                                                                  \
   case M:                                                                                              \
     hipLaunchKernelGGL((k6::scan_mfma6_kernel<RFX_BF16, 10, 768, M>), grid, dim3(512), 0, st, Xh, Qh, nq, \
-                       ntiles, tau, cs, cr, p.n_lists, nullptr);                                       \
+                       ntiles, tau, cs, cr, p.n_lists, nullptr, nullptr);                                       \
     break;
   switch (mode) {
     RFX_K6_DBG(1)

@@ -135,7 +135,10 @@ template <int DT, int KL, int D, int MODE = 0, int RING = kRing>
 __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Qp,
                                                             int nq, int ntiles, uint32_t* __restrict__ tau,
                                                             float* __restrict__ cand_s, int* __restrict__ cand_r,
-                                                            int64_t n_lists, const uint32_t* __restrict__ mask) {
+                                                            int64_t n_lists, const uint32_t* __restrict__ mask,
+                                                            const uint32_t* __restrict__ gate) {
+  // gate (the two-pass scan's fallback, k_screen.hip): run only when the screen asked for it
+  if (gate && *gate == 0u) return;
   constexpr int NKS = D / 32;   // 32-deep k-steps per tile
   constexpr int NST = D / kSK;  // stages per tile
   constexpr int KPS = kSK / 32;  // k-steps per stage (8)
@@ -378,19 +381,19 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
 // one translation unit per (dtype, D) instantiates the kernel for the lane-list sizes KL in {4, 10}
 #define RFX_K6_INSTANTIATE(DTV, DV, NAME)                                                                  \
   int NAME(int kl, dim3 grid, hipStream_t st, const uint16_t* X, const uint16_t* Qp, int nq, int ntiles,     \
-           uint32_t* tau, float* cs, int* cr, int64_t n_lists, const uint32_t* mask) {                      \
+           uint32_t* tau, float* cs, int* cr, int64_t n_lists, const uint32_t* mask, const uint32_t* gate) {  \
     if (kl == 4 && !mask)                                                                                \
       hipLaunchKernelGGL((scan_mfma6_kernel<DTV, 4, DV>), grid, dim3(512), 0, st, X, Qp, nq, ntiles, tau, cs, \
-                         cr, n_lists, mask);                                                              \
+                         cr, n_lists, mask, gate);                                                              \
     else if (kl == 10 && !mask)                                                                          \
       hipLaunchKernelGGL((scan_mfma6_kernel<DTV, 10, DV>), grid, dim3(512), 0, st, X, Qp, nq, ntiles, tau,  \
-                         cs, cr, n_lists, mask);                                                          \
+                         cs, cr, n_lists, mask, gate);                                                          \
     else if (kl == 4)                                                                                    \
       hipLaunchKernelGGL((scan_mfma6_kernel<DTV, 4, DV, kModeMask>), grid, dim3(512), 0, st, X, Qp, nq,     \
-                         ntiles, tau, cs, cr, n_lists, mask);                                             \
+                         ntiles, tau, cs, cr, n_lists, mask, gate);                                             \
     else if (kl == 10)                                                                                   \
       hipLaunchKernelGGL((scan_mfma6_kernel<DTV, 10, DV, kModeMask>), grid, dim3(512), 0, st, X, Qp, nq,    \
-                         ntiles, tau, cs, cr, n_lists, mask);                                             \
+                         ntiles, tau, cs, cr, n_lists, mask, gate);                                             \
     else                                                                                                 \
       return -1;                                                                                         \
     return 0;                                                                                            \

@@ -89,7 +89,9 @@ __global__ __launch_bounds__(512, 1) void scan_mfma8_kernel(const uint16_t* __re
                                                             int nq, int ntiles, int ranges, int groups, int paired,
                                                             uint32_t* __restrict__ tau, float* __restrict__ cand_s,
                                                             int* __restrict__ cand_r, int64_t n_lists,
-                                                            const uint32_t* __restrict__ mask, int mask_words) {
+                                                            const uint32_t* __restrict__ mask, int mask_words,
+                                                            const uint32_t* __restrict__ gate) {
+  if (gate && *gate == 0u) return;  // the two-pass scan's gated fallback (k_screen.hip)
   constexpr int NST = D / kSK;   // stages per tile (8)
   constexpr int KPS = kSK / 32;  // k-steps per stage (4); a wave runs 2 of them
   constexpr int KW = KPS / 2;    // k-steps per stage per wave
@@ -287,11 +289,11 @@ __global__ __launch_bounds__(512, 1) void scan_mfma8_kernel(const uint16_t* __re
   }
 }
 
-#define RFX_K8_ARGS X, Qp, nq, ntiles, ranges, groups, paired, tau, cs, cr, n_lists, mask, mask_words
+#define RFX_K8_ARGS X, Qp, nq, ntiles, ranges, groups, paired, tau, cs, cr, n_lists, mask, mask_words, gate
 #define RFX_K8_INSTANTIATE(DTV, DV, NAME)                                                                 \
   int NAME(int kl, dim3 grid, hipStream_t st, const uint16_t* X, const uint16_t* Qp, int nq, int ntiles,     \
            int ranges, int groups, int paired, uint32_t* tau, float* cs, int* cr, int64_t n_lists,        \
-           const uint32_t* mask, int mask_words) {                                                        \
+           const uint32_t* mask, int mask_words, const uint32_t* gate) {                                  \
     if (kl == 4 && mask)                                                                                \
       hipLaunchKernelGGL((scan_mfma8_kernel<DTV, 4, DV, kModeMask>), grid, dim3(512), 0, st, RFX_K8_ARGS);  \
     else if (kl == 10 && mask)                                                                          \

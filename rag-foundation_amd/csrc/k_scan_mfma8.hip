@@ -7,7 +7,7 @@ namespace k8 {
 #define RFX_K8_DECL(NAME)                                                                                 \
   int NAME(int kl, dim3 grid, hipStream_t st, const uint16_t* X, const uint16_t* Qp, int nq, int ntiles,     \
            int ranges, int groups, int paired, uint32_t* tau, float* cs, int* cr, int64_t n_lists,        \
-           const uint32_t* mask, int mask_words);
+           const uint32_t* mask, int mask_words, const uint32_t* gate);
 RFX_K8_DECL(launch_bf16_1024)
 RFX_K8_DECL(launch_f16_1024)
 #undef RFX_K8_DECL
@@ -38,7 +38,7 @@ MfmaPlan plan_scan_mfma8(int64_t nrows, int D, int dtype, int64_t nq, int k) {
 }
 
 int launch_scan_mfma8(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask) {
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask, const uint32_t* gate) {
   if (!p.ok || D != 1024) return -1;
   const int ntiles = (nrows + k8::kTM - 1) / k8::kTM;
   if (hipMemsetAsync(tau, 0, tau_bytes_mfma8(p), st) != hipSuccess) return -2;
@@ -46,7 +46,7 @@ int launch_scan_mfma8(const MfmaPlan& p, const void* X, int nrows, int D, int dt
   dim3 grid(p.blocks * p.q_blocks);
   auto f = dtype == RFX_BF16 ? k8::launch_bf16_1024 : k8::launch_f16_1024;
   return f(p.k_lane, grid, st, (const uint16_t*)X, (const uint16_t*)Qpad, nq, ntiles, p.blocks, p.q_blocks,
-           paired, tau, cs, cr, p.n_lists, mask, (nrows + 31) / 32);
+           paired, tau, cs, cr, p.n_lists, mask, (nrows + 31) / 32, gate);
 }
 
 }  // namespace rfx

@@ -1,0 +1,331 @@
+// k_scan_screen.h — kernel 10, the int8 screen of the exact two-pass scan (BASELINE config 3:
+// 10M×768 bf16, nq 256, k 10; config 4's shard at d 1024).
+//
+// Path: the retrieval half of GeminiRag.ask_stream (backend/app/services/gemini_rag.py:517-551).
+// The screen reads an int8 copy of the store (half the bytes of the bf16 rows) on
+// v_mfma_i32_16x16x64_i8 (twice the bf16 rate) and keeps, per query, every row whose exact score
+// can still reach the query's k-th best; k_screen.hip re-scores those rows exactly from the bf16
+// rows and returns the same top-k as the exact scan (kernel 6 / 8).  DESIGN §4.10.
+//
+// Why the result is exact.  Rows are quantised per 32-row tile (scale s_t = amax_t / 127, codes
+// c = rint(x / s_t)), queries per query (s_y).  For a row x and query y with reconstructions
+// x^ = s_t c_x, y^ = s_y c_y:   x·y − x^·y^ = x·(y − y^) + (x − x^)·y^, so by Cauchy-Schwarz
+//     |x·y − s_t s_y D| <= ||x|| ||y − y^|| + ||x − x^|| ||y^|| =: E_q      (D = c_x·c_y, exact i32)
+// with ||x|| and ||x − x^|| replaced by their maxima over the store (the `stats` of the
+// quantiser, rounded up).  In units of s_y the screen score is A = s_t D (one f32 rounding,
+// covered by the slack in e2 = 2 E_q / s_y rounded up, k_screen.hip quantize_queries_kernel).
+// Let a_k be the k-th best A over live rows.  The k rows that reach it have exact scores
+// >= a_k − E_q, so the true k-th best exact score is too, and a row of the true top-k has
+// A >= a_k − 2 E_q / s_y = a_k − e2.  The kernel keeps every such row:
+//   * pruning.  Kernel 6's bound (own list's KL-th best, the cross-workgroup slot table) is a lower
+//     bound of a_k (KL >= k); a row is looked at only when A >= bound − e2;
+//   * lists.  Each lane keeps the KL best A of the rows it looked at (LDS, as kernel 6) and the
+//     best A it had to drop (`drop`: not inserted, or evicted).  k_screen.hip's select kernel
+//     finds a_k from the lists' union, and takes the fallback (the exact kernel on the whole
+//     batch) when a dropped A reaches a_k − e2 or the survivors overflow its buffer.
+// Dead rows (tombstones, the NaN tail, rows a metadata filter excludes) carry code 0 and a clear
+// bit in the tile's live word; the slow path skips them, so they never raise a_k.
+//
+// Layout and schedule follow kernel 6 (k_scan_mfma6.h) at half the bytes: workgroup = 8 waves ×
+// 32 resident queries (B fragments: D / 64 k-steps × 2 query blocks × 16 B = 96 VGPRs at d 768),
+// 32-row tiles (block b takes tiles b, b + B, ...), a stage = 32 rows × 256 codes (8 KB) by LDS-DMA
+// into a RING-slot ring (one 1-KB piece per wave per stage), LDS image with chunk c of row r at
+// c ^ (r & 15), counted vmcnt + s_barrier per stage, v_permlane16_swap epilogue.
+// Algorithmic bytes per tile: 32 * D (codes) + 8 (tile scale, live word).
+#pragma once
+#include "k_mfma_common.h"
+
+namespace rfx {
+namespace k10 {
+
+using namespace mfc;
+
+constexpr int kWaves = 8;
+constexpr int kTM = 32;                   // rows per tile
+constexpr int kQW = 32;                   // queries per wave
+constexpr int kQG = kWaves * kQW;         // 256 queries per workgroup
+constexpr int kSK = 256;                  // codes (bytes) per row per stage
+constexpr int kRowB = kSK;                // 256 B per row per stage
+constexpr int kSlot = kTM * kRowB;        // 8 KB: 32 rows × 256 codes
+#ifndef RFX_K10_RING
+#define RFX_K10_RING 8
+#endif
+constexpr int kRing = RFX_K10_RING;       // slots; RING - 1 stages in flight
+constexpr int kGPW = 1;                   // LDS-DMA pieces per wave per stage (8 KB / 1 KB / 8 waves)
+constexpr int kTauW = 16;                 // u32 per query in the threshold table (KL <= 10 used)
+constexpr int kTauBytes = kQG * kTauW * 4;  // 16 KB
+constexpr int kTauGPW = kTauBytes / 1024 / kWaves;
+template <int RING>
+constexpr int tau_off() { return RING * kSlot; }
+template <int RING>
+constexpr int list_off() { return tau_off<RING>() + kTauBytes; }
+template <int KL, int RING>
+constexpr int lds_bytes() { return list_off<RING>() + kWaves * KL * 64 * 8; }
+static_assert(lds_bytes<10, 12>() <= 163840, "LDS budget");
+static_assert(kSlot / 1024 == kWaves * kGPW && kTauGPW == 2, "DMA pieces per wave");
+
+__device__ __forceinline__ bool tau_refresh_tile(int it) { return it < 2 || (it & 3) == 3; }
+
+__device__ __forceinline__ v4i32 mfma_i8(const uint4& a, const uint4& b, const v4i32& c) {
+  return __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(v4i32, a), __builtin_bit_cast(v4i32, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b), c); }
+
+// Fold one tile's 16 values of this lane (rows rbase + (r & 7) + 16 (r >> 3), ROWMAP 1 of
+// k_mfma_common.h) into its list.  thr_o: the pruning bound (orderable A, 0 = none); rows are
+// looked at from thr − e2 on.  drop_o: the best A this lane looked at and did not keep.
+template <int KL>
+__device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint32_t bits, uint64_t* Ls, uint32_t& thr_o,
+                                            float e2, uint32_t& drop_o, int rbase, v4i32 tau_rsrc, uint32_t slot_voff) {
+  int mx = max3i(a[0][0], a[0][1], a[0][2]);
+  mx = max3i(mx, a[0][3], a[1][0]);
+  mx = max3i(mx, a[1][1], a[1][2]);
+  mx = max3i(mx, a[1][3], a[2][0]);
+  mx = max3i(mx, a[2][1], a[2][2]);
+  mx = max3i(mx, a[2][3], a[3][0]);
+  mx = max3i(mx, a[3][1], a[3][2]);
+  mx = max(mx, a[3][3]);
+  const float thr = thr_o ? unord(thr_o) - e2 : -__builtin_inff();
+  if ((float)mx * st >= thr) {  // s_t >= 0: the tile's best A bounds every row's
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float s = (float)a[r >> 2][r & 3] * st;
+      if (((bits >> ((r & 7) + 16 * (r >> 3))) & 1u) && s >= thr) {
+        const int row = rbase + (r & 7) + 16 * (r >> 3);
+        const uint64_t key = ((uint64_t)ord(s) << 32) | (uint32_t)(~(uint32_t)row);
+        const uint64_t last = Ls[(KL - 1) * 64];
+        if (key > last) {
+          if (last) drop_o = max(drop_o, (uint32_t)(last >> 32));  // evicted
+          int i = KL - 1;
+          for (; i > 0; --i) {
+            const uint64_t prev = Ls[(i - 1) * 64];
+            if (prev >= key) break;
+            Ls[i * 64] = prev;
+          }
+          Ls[i * 64] = key;
+        } else {
+          drop_o = max(drop_o, ord(s));  // looked at, not kept
+        }
+      }
+    }
+    const uint32_t own = (uint32_t)(Ls[(KL - 1) * 64] >> 32);
+    thr_o = own > thr_o ? own : thr_o;
+    batomic_umax(tau_rsrc, slot_voff, (uint32_t)(Ls[0] >> 32));
+  }
+}
+
+// X: int8 codes [ntiles * 32][D]; tscale / live: per tile; Qc: int8 query codes [nq_pad][D];
+// qe2: [nq_pad] e2 per query (units of the query's scale).  Outputs per (query, list): KL
+// candidates (A, row) sorted best first, empty tail (-inf, kEmptyRow), and the list's drop.
+template <int KL, int D, bool MASK, int RING = kRing>
+__global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const float* __restrict__ tscale,
+                                                             const uint32_t* __restrict__ live, const int8_t* __restrict__ Qc,
+                                                             const float* __restrict__ qe2, int nq, int ntiles,
+                                                             uint32_t* __restrict__ tau, float* __restrict__ cand_s,
+                                                             int* __restrict__ cand_r, uint32_t* __restrict__ drops,
+                                                             int64_t n_lists, const uint32_t* __restrict__ mask) {
+  constexpr int NKS = D / 64;    // 64-deep k-steps per tile
+  constexpr int NST = D / kSK;   // stages per tile
+  constexpr int KPS = kSK / 64;  // k-steps per stage (4)
+  static_assert(D % kSK == 0, "D must be a multiple of 256");
+  static_assert(KL <= 10, "threshold table holds 10 slots");
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[lds_bytes<KL, RING>()];
+  constexpr int kTauOff = tau_off<RING>();
+  constexpr int kListOff = list_off<RING>();
+
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, lane = tid & 63;
+  const int half = lane >> 5;
+  const int range = blockIdx.x;
+  const int qg = blockIdx.y * kQG;
+  const int q = qg + w * kQW + 16 * ((lane >> 4) & 1) + (lane & 15);  // after the pair swap
+  const int nblk = gridDim.x;
+  const int nt = range < ntiles ? (ntiles - range + nblk - 1) / nblk : 0;
+  const int S = nt * NST;
+  if (S == 0) return;
+  const int lst = range * 2 + half;
+  const float e2 = qe2[q];
+
+  {
+    uint4* tz = (uint4*)(lds + kTauOff);
+#pragma unroll
+    for (int i = 0; i < kTauBytes / 16 / 512; ++i) tz[tid + 512 * i] = uint4{0u, 0u, 0u, 0u};
+  }
+  uint64_t* const Ls = (uint64_t*)(lds + kListOff) + (w * KL) * 64 + lane;
+#pragma unroll
+  for (int i = 0; i < KL; ++i) Ls[i * 64] = 0ull;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // resident query codes (B[k][col] of 16x16x64 i8): query block qb, lane holds col 16 qb + (lane & 15),
+  // k = 64 ks + 16 (lane >> 4) + j; the A fragments below use the same k map, so the i32 dot is exact
+  uint4 bq[2 * NKS];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int8_t* qa = Qc + (int64_t)(qg + w * kQW + 16 * qb + (lane & 15)) * D + 16 * (lane >> 4);
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) bq[2 * ks + qb] = *(const uint4*)(qa + 64 * ks);
+  }
+
+  // LDS-DMA piece of wave w: slot bytes [1024 w, +1024) = rows 4w .. 4w+3 (256 B each); lane ->
+  // (row 4w + (lane >> 4), position lane & 15) <- source chunk position ^ (row & 15)
+  const int pr = 4 * w + (lane >> 4);
+  const uint32_t laneoff = (uint32_t)(pr * D + (((lane & 15) ^ (pr & 15)) * 16));
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
+  const int64_t tile_stride = (int64_t)nblk * kTM * D;
+  auto issue_piece = [&](int gi, int slot) {
+    gi = gi < S ? gi : S - 1;  // tail: harmless duplicate loads keep the counted waits exact
+    const int ti = gi / NST;
+    const int si = gi - ti * NST;
+    const int8_t* tbase = X + (int64_t)range * kTM * D + ti * tile_stride + si * kSK;
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)(slot * kSlot) + (uint32_t)(w * 1024));
+    bdma_nt(make_rsrc(tbase), laneoff, dst);  // codes are read once per batch
+  };
+  const v4i32 tau_rsrc = make_rsrc(tau);
+  auto issue_tau = [&]() {
+#pragma unroll
+    for (int u = 0; u < kTauGPW; ++u) {
+      const int i = w + kWaves * u;
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + kTauOff + i * 1024);
+      bdma_sc1(tau_rsrc, (uint32_t)(qg * kTauW * 4 + tid * 16 + u * kWaves * 1024), dst);
+    }
+  };
+
+  uint32_t thr = 0u, drop = 0u;
+  const uint32_t slot_voff = (uint32_t)(q * kTauW + lst % KL) * 4u;
+  const uint8_t* const tq = lds + kTauOff + (w * kQW + (lane & 15) + 16 * ((lane >> 4) & 1)) * (kTauW * 4);
+  // A fragment of row block rb, k-step kk of a slot: row 16 rb + (lane & 15), chunk 4 kk + (lane >> 4)
+  const uint8_t* const frag_base = lds + (lane & 15) * kRowB;
+  const int sw = lane & 15;
+  struct Frag {
+    uint4 a[2];
+  };
+  auto read_frag = [&](int slot, int kk) -> Frag {
+    const uint8_t* p = frag_base + slot * kSlot + (((4 * kk + (lane >> 4)) ^ sw) << 4);
+    Frag f;
+    f.a[0] = *(const uint4*)p;
+    f.a[1] = *(const uint4*)(p + 16 * kRowB);
+    return f;
+  };
+
+  // Schedule: stage h's piece goes out at k-step 0 of stage h - (RING - 1) into the slot freed at
+  // stage h - RING's barrier; fragments are read one k-step ahead; the stage-end wait + barrier sit
+  // at k-step KPS - 1.
+  constexpr int PF = 1;
+  constexpr int NF = PF + 1;
+  constexpr int KB = KPS - PF;
+  constexpr int AHEAD = RING - 1;
+  constexpr int YNG = (RING - 2) * kGPW;  // ops younger than the next stage
+  static_assert((NST * KPS) % NF == 0, "fragment rotation must realign every tile");
+
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  issue_tau();
+#pragma unroll
+  for (int p = 0; p < AHEAD; ++p) issue_piece(p, p);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(YNG) : "memory");
+  asm volatile("s_barrier" ::: "memory");
+
+  Frag fr[NF];
+  fr[0] = read_frag(0, 0);
+  v4i32 acc4[4];  // [rb * 2 + qb]
+  for (int it = 0; it < nt; ++it) {
+    const int tile = range + it * nblk;
+    const int gbase = it * NST;
+    // per-tile scale and live word: scalar loads, consumed in the epilogue
+    const float st = tscale[tile];
+    uint32_t lw = live[tile];
+    if constexpr (MASK) lw &= mask[tile];
+    if (it >= 2 && tau_refresh_tile(it - 2)) thr = max(thr, tau_min<KL>(tq));
+    auto young = [&](int s) {
+      const int dmax = (RING - 3 + NST - s) / NST;
+      bool y = false;
+#pragma unroll
+      for (int d = 1; d <= dmax; ++d) y = y || (it >= d && tau_refresh_tile(it - d));
+      return y;
+    };
+#pragma unroll
+    for (int s = 0; s < NST; ++s) {
+      const int g = gbase + s;
+      const int slot = g % RING;
+#pragma unroll
+      for (int kk = 0; kk < KPS; ++kk) {
+        if (kk == 0) issue_piece(g + RING - 1, (g + RING - 1) % RING);
+        if (kk == KB) {
+          if (young(s))
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(YNG + kTauGPW) : "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(YNG) : "memory");
+          asm volatile("s_barrier" ::: "memory");
+          if (s == NST - 1 && tau_refresh_tile(it)) issue_tau();
+        }
+        const int ks = s * KPS + kk;
+        fr[(ks + PF) % NF] = kk + PF < KPS ? read_frag(slot, kk + PF) : read_frag((g + 1) % RING, kk + PF - KPS);
+        const Frag& cur = fr[ks % NF];
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int qb = 0; qb < 2; ++qb)
+            acc4[2 * rb + qb] = ks == 0 ? mfma_i8(cur.a[rb], bq[2 * ks + qb], v4i32{0, 0, 0, 0})
+                                        : mfma_i8(cur.a[rb], bq[2 * ks + qb], acc4[2 * rb + qb]);
+      }
+    }
+
+    // epilogue: pair swap (even 16-lane row keeps query n, odd keeps 16 + n), then fold
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const auto r = __builtin_amdgcn_permlane16_swap((uint32_t)acc4[2 * rb][i], (uint32_t)acc4[2 * rb + 1][i], false, false);
+        acc4[2 * rb][i] = (int)r[0];
+        acc4[2 * rb + 1][i] = (int)r[1];
+      }
+    fold_screen<KL>(acc4, st, lw >> (8 * half), Ls, thr, e2, drop, tile * kTM + 8 * half, tau_rsrc, slot_voff);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (q < nq) {
+    // entries below (the query's bound as it stands now) − e2 cannot be survivors: dropped here
+    uint32_t m = 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < KL; ++j)
+      m = min(m, __hip_atomic_load(tau + (int64_t)q * kTauW + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    const uint32_t fin = max(thr, m);
+    const float lo = fin ? unord(fin) - e2 : -__builtin_inff();
+    const int64_t o = ((int64_t)q * n_lists + lst) * KL;
+#pragma unroll
+    for (int i = 0; i < KL; ++i) {
+      const uint64_t key = Ls[i * 64];
+      const float sc = unord((uint32_t)(key >> 32));
+      const bool keep = key && sc >= lo;
+      cand_s[o + i] = keep ? sc : -__builtin_inff();
+      cand_r[o + i] = keep ? (int)(~(uint32_t)key) : kEmptyRow;
+    }
+    drops[(int64_t)q * n_lists + lst] = drop;
+  }
+}
+
+// one translation unit per D instantiates the kernel for KL in {4, 10}, with and without a filter mask
+#define RFX_K10_INSTANTIATE(DV, NAME)                                                                         \
+  int NAME(int kl, dim3 grid, hipStream_t st, const int8_t* X, const float* ts, const uint32_t* lv,           \
+           const int8_t* Qc, const float* qe2, int nq, int ntiles, uint32_t* tau, float* cs, int* cr,          \
+           uint32_t* dr, int64_t n_lists, const uint32_t* mask) {                                            \
+    if (kl == 4 && !mask)                                                                                   \
+      hipLaunchKernelGGL((scan_screen_kernel<4, DV, false>), grid, dim3(512), 0, st, X, ts, lv, Qc, qe2, nq,   \
+                         ntiles, tau, cs, cr, dr, n_lists, mask);                                            \
+    else if (kl == 10 && !mask)                                                                             \
+      hipLaunchKernelGGL((scan_screen_kernel<10, DV, false>), grid, dim3(512), 0, st, X, ts, lv, Qc, qe2, nq,  \
+                         ntiles, tau, cs, cr, dr, n_lists, mask);                                            \
+    else if (kl == 4)                                                                                       \
+      hipLaunchKernelGGL((scan_screen_kernel<4, DV, true>), grid, dim3(512), 0, st, X, ts, lv, Qc, qe2, nq,    \
+                         ntiles, tau, cs, cr, dr, n_lists, mask);                                            \
+    else if (kl == 10)                                                                                      \
+      hipLaunchKernelGGL((scan_screen_kernel<10, DV, true>), grid, dim3(512), 0, st, X, ts, lv, Qc, qe2, nq,   \
+                         ntiles, tau, cs, cr, dr, n_lists, mask);                                            \
+    else                                                                                                    \
+      return -1;                                                                                            \
+    return 0;                                                                                               \
+  }
+
+}  // namespace k10
+}  // namespace rfx

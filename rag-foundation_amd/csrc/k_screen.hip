@@ -1,0 +1,444 @@
+// k_screen.hip — the exact two-pass scan around kernel 10 (k_scan_screen.h): the int8 copy of the
+// store (per-tile quantiser), the per-batch query quantiser, and the select kernel that finds each
+// query's survivors, re-scores them exactly from the stored rows and writes the top-k.  DESIGN §4.10.
+//
+// Path: the retrieval half of GeminiRag.ask_stream (backend/app/services/gemini_rag.py:517-551);
+// the store write of upload_file (gemini_rag.py:307-352) keeps the int8 copy current.
+// oracle/screen.py restates every step; the codes, tile scales and live words are bit-exact with it
+// (one correctly rounded IEEE op per float step: __fdiv_rn, rintf).
+#include "k_scan_screen.h"
+
+namespace rfx {
+namespace k10 {
+#define RFX_K10_DECL(NAME)                                                                                    \
+  int NAME(int kl, dim3 grid, hipStream_t st, const int8_t* X, const float* ts, const uint32_t* lv,           \
+           const int8_t* Qc, const float* qe2, int nq, int ntiles, uint32_t* tau, float* cs, int* cr,          \
+           uint32_t* dr, int64_t n_lists, const uint32_t* mask);
+RFX_K10_DECL(launch_768)
+RFX_K10_DECL(launch_1024)
+#undef RFX_K10_DECL
+}  // namespace k10
+
+namespace {
+
+using mfc::ord;
+using mfc::unord;
+
+struct Rec {  // the merge records of rfx/dist.py pack(): {f32 score, i32 pad, i64 row}
+  float s;
+  int pad;
+  long long r;
+};
+
+template <int DT>
+__device__ __forceinline__ float widen(uint16_t h) {
+  if constexpr (DT == RFX_BF16)
+    return __uint_as_float((uint32_t)h << 16);
+  else
+    return f16_to_f32(h);
+}
+
+// f64 -> f32 rounded up (an upper bound stays an upper bound)
+__device__ __forceinline__ float f32_up(double v) {
+  float f = (float)v;
+  if ((double)f < v) f = nextafterf(f, __builtin_inff());
+  return f;
+}
+
+__device__ __forceinline__ int8_t code_of(float x, float s) {
+  const float c = rintf(__fdiv_rn(x, s));
+  return (int8_t)fminf(fmaxf(c, -127.f), 127.f);
+}
+
+// ---- the int8 copy: one 256-thread block per 32-row tile ----------------------------------------
+// thread t: row t >> 3, segment t & 7 (D / 8 elements).  A row is dead (tombstone, NaN tail) when any
+// element is NaN: code 0, live bit clear, excluded from the scale.  s_t = amax / 127 over the live
+// rows (0 for a tile without any), c = clamp(rint(x / s_t), ±127).  stats[0] / stats[1] grow to the
+// max over live rows of ||x|| and ||x − s_t c|| (f64 sums, rounded up to f32, atomicMax on the bits).
+template <int DT, int D>
+__global__ __launch_bounds__(256) void screen_quantize_kernel(const uint16_t* __restrict__ X, int64_t tile0,
+                                                              const int64_t* __restrict__ tiles,
+                                                              int8_t* __restrict__ codes, float* __restrict__ tscale,
+                                                              uint32_t* __restrict__ live, uint32_t* __restrict__ stats) {
+  constexpr int PER = D / 8;
+  const int64_t tile = tiles ? tiles[blockIdx.x] : tile0 + blockIdx.x;
+  const int t = threadIdx.x, row = t >> 3, seg = t & 7;
+  const int64_t r = tile * 32 + row;
+  const uint16_t* xr = X + r * D + seg * PER;
+  __shared__ float wmax[4];
+  __shared__ uint32_t word;
+  if (t == 0) word = 0u;
+  bool nan = false;
+  float am = 0.f;
+#pragma unroll 4
+  for (int i = 0; i < PER; i += 8) {
+    const uint4 v = *(const uint4*)(xr + i);
+    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float f = widen<DT>((uint16_t)(e & 1 ? u[e >> 1] >> 16 : u[e >> 1] & 0xffffu));
+      nan |= f != f;
+      am = fmaxf(am, fabsf(f));
+    }
+  }
+  // the 8 threads of a row are 8 consecutive lanes of one wave
+  int dead = nan;
+  dead |= __shfl_xor(dead, 1);
+  dead |= __shfl_xor(dead, 2);
+  dead |= __shfl_xor(dead, 4);
+  float m = dead ? 0.f : am;
+#pragma unroll
+  for (int off = 32; off; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+  if ((t & 63) == 0) wmax[t >> 6] = m;
+  __syncthreads();
+  const float amax = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+  const float s = amax > 0.f ? __fdiv_rn(amax, 127.f) : 0.f;
+  double xx = 0.0, ee = 0.0;
+  int8_t* cw = codes + r * D + seg * PER;
+#pragma unroll 4
+  for (int i = 0; i < PER; i += 8) {
+    const uint4 v = *(const uint4*)(xr + i);
+    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+    uint32_t pk[2] = {0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float f = widen<DT>((uint16_t)(e & 1 ? u[e >> 1] >> 16 : u[e >> 1] & 0xffffu));
+      const int8_t c = (!dead && s > 0.f) ? code_of(f, s) : (int8_t)0;
+      pk[e >> 2] |= (uint32_t)(uint8_t)c << (8 * (e & 3));
+      if (!dead) {
+        const double d = (double)f - (double)s * (double)c;  // exact: both terms fit 53 bits
+        xx += (double)f * (double)f;
+        ee += d * d;
+      }
+    }
+    *(uint2*)(cw + i) = uint2{pk[0], pk[1]};
+  }
+  xx += __shfl_xor(xx, 1);
+  xx += __shfl_xor(xx, 2);
+  xx += __shfl_xor(xx, 4);
+  ee += __shfl_xor(ee, 1);
+  ee += __shfl_xor(ee, 2);
+  ee += __shfl_xor(ee, 4);
+  if (seg == 0 && !dead) {
+    atomicMax(stats + 0, __float_as_uint(f32_up(sqrt(xx))));  // non-negative floats order as u32
+    atomicMax(stats + 1, __float_as_uint(f32_up(sqrt(ee))));
+    atomicOr(&word, 1u << row);
+  }
+  __syncthreads();
+  if (t == 0) {
+    tscale[tile] = s;
+    live[tile] = word;
+  }
+}
+
+// ---- per batch: query codes and e2 (one wave per query) -------------------------------------------
+// s_y = amax / 127, c = clamp(rint(y / s_y)); E_q = Xmax ||y − s_y c|| + Emax ||s_y c|| (Cauchy-Schwarz,
+// k_scan_screen.h); e2 = (2 E_q + 4e-7 (Xmax + Emax) ||s_y c||) (1 + 1e-5) / s_y rounded up: the
+// 4e-7 term covers the f32 roundings of A = s_t D (2^-24 relative, twice) and of the bound
+// subtraction, the 1e-5 the f64 norms.  Also zeroes the query's threshold slots and (block 0) the
+// fallback gate.  Padded queries (q >= nq) get code 0 and e2 0.
+template <int DT, int D>
+__global__ __launch_bounds__(256) void screen_queries_kernel(const uint16_t* __restrict__ Q, int nq, int nq_pad,
+                                                             int8_t* __restrict__ Qc, float* __restrict__ qe2,
+                                                             const uint32_t* __restrict__ stats,
+                                                             uint32_t* __restrict__ tau, uint32_t* __restrict__ gate) {
+  constexpr int NM = D / 256;
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *gate = 0u;
+  if (q >= nq_pad) return;
+  if (lane < k10::kTauW) tau[(int64_t)q * k10::kTauW + lane] = 0u;
+  float y[NM][4];
+  float am = 0.f;
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    uint2 v = uint2{0u, 0u};
+    if (q < nq) v = *(const uint2*)(Q + (int64_t)q * D + 256 * m + 4 * lane);
+    const uint32_t u[2] = {v.x, v.y};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      y[m][e] = widen<DT>((uint16_t)(e & 1 ? u[e >> 1] >> 16 : u[e >> 1] & 0xffffu));
+      am = fmaxf(am, fabsf(y[m][e]));
+    }
+  }
+#pragma unroll
+  for (int off = 32; off; off >>= 1) am = fmaxf(am, __shfl_xor(am, off));
+  const float s = am > 0.f ? __fdiv_rn(am, 127.f) : 0.f;
+  double ey = 0.0;
+  long long cc = 0;
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    uint32_t pk = 0u;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int8_t c = s > 0.f ? code_of(y[m][e], s) : (int8_t)0;
+      pk |= (uint32_t)(uint8_t)c << (8 * e);
+      const double d = (double)y[m][e] - (double)s * (double)c;
+      ey += d * d;
+      cc += (long long)c * c;
+    }
+    *(uint32_t*)(Qc + (int64_t)q * D + 256 * m + 4 * lane) = pk;
+  }
+#pragma unroll
+  for (int off = 32; off; off >>= 1) {
+    ey += __shfl_xor(ey, off);
+    cc += __shfl_xor(cc, off);
+  }
+  if (lane == 0) {
+    float e2 = 0.f;
+    if (s > 0.f) {
+      const double xm = (double)__uint_as_float(stats[0]), em = (double)__uint_as_float(stats[1]);
+      const double yh = (double)s * sqrt((double)cc);
+      const double eq = xm * sqrt(ey) + em * yh;
+      e2 = f32_up((2.0 * eq + 4e-7 * (xm + em) * yh) * (1.0 + 1e-5) / (double)s);
+    }
+    qe2[q] = e2;
+  }
+}
+
+// ---- select: survivors, exact re-score, top-k (one 512-thread block per query) --------------------
+constexpr int kSelCap = 2048;  // kept candidates per query held in LDS; more -> fallback
+
+template <int DT, int D>
+__global__ __launch_bounds__(512) void screen_select_kernel(const float* __restrict__ cs, const int* __restrict__ cr,
+                                                            const uint32_t* __restrict__ drops, int64_t n_lists,
+                                                            int list_len, const float* __restrict__ qe2,
+                                                            const uint16_t* __restrict__ Q,
+                                                            const uint16_t* __restrict__ X, int k, int64_t row_offset,
+                                                            float* __restrict__ out_s, int64_t* __restrict__ out_r,
+                                                            Rec* __restrict__ out_rec, uint32_t* __restrict__ gate,
+                                                            int* __restrict__ diag, int force) {
+  constexpr int NT = 512, NW = NT / 64, NM = D / 256, U = 4;
+  __shared__ float ca[kSelCap];   // screen score A of kept candidate i
+  __shared__ int crow[kSelCap];   // its row
+  __shared__ int sv[kSelCap];     // survivor j -> candidate index
+  __shared__ double sx[kSelCap];  // survivor j's exact score
+  __shared__ int n_c, n_sv, n_ok, fail;
+  __shared__ float ak;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int64_t q = blockIdx.x;
+  if (tid == 0) {
+    n_c = n_sv = n_ok = fail = 0;
+    ak = -__builtin_inff();
+  }
+  __syncthreads();
+  // 1. compact the kept candidates (the scan wrote -inf for empty slots and dropped entries)
+  const int64_t n = n_lists * list_len;
+  const float* qs = cs + q * n;
+  const int* qr = cr + q * n;
+  for (int64_t b = tid; b < n; b += (int64_t)NT * U) {
+    float s[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) s[u] = b + u * NT < n ? qs[b + u * NT] : -__builtin_inff();
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (s[u] != -__builtin_inff()) {
+        const int i = atomicAdd(&n_c, 1);
+        if (i < kSelCap) {
+          ca[i] = s[u];
+          crow[i] = qr[b + u * NT];
+        }
+      }
+  }
+  __syncthreads();
+  const int nc = n_c;
+  if (nc > kSelCap || force) fail = 1;
+  const int ncl = nc < kSelCap ? nc : kSelCap;
+  // 2. a_k = the k-th best A (with multiplicity): the value v with #{> v} < k <= #{>= v}
+  for (int i = tid; i < ncl; i += NT) {
+    const float si = ca[i];
+    int gt = 0, ge = 0;
+    for (int j = 0; j < ncl; ++j) {
+      const float sj = ca[j];
+      gt += sj > si;
+      ge += sj >= si;
+    }
+    if (gt < k && ge >= k) ak = si;  // every writer writes the same value
+  }
+  __syncthreads();
+  const float e2 = qe2[q];
+  const float t = ncl >= k ? ak - e2 : -__builtin_inff();
+  const uint32_t ot = ord(t);
+  // 3. a row dropped at or above t could be a survivor the lists lost: fallback
+  for (int64_t j = tid; j < n_lists; j += NT) {
+    const uint32_t d = drops[q * n_lists + j];
+    if (d && d >= ot) fail = 1;
+  }
+  for (int i = tid; i < ncl; i += NT)
+    if (ca[i] >= t) sv[atomicAdd(&n_sv, 1)] = i;
+  __syncthreads();
+  if (fail) {
+    if (tid == 0) __hip_atomic_store(gate, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (diag && tid == 0) {
+      diag[q * 2] = nc;
+      diag[q * 2 + 1] = -1;
+    }
+    return;  // the gated exact pass rewrites the whole batch
+  }
+  const int ns = n_sv;
+  // 4. exact re-score: lane holds query elements 256 m + 4 lane + e; f32 products of bf16 / f16
+  // values are exact, their sum is taken in f64 (the oracle's f64 dot up to f64 rounding)
+  float y[NM][4];
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    const uint2 v = *(const uint2*)(Q + q * D + 256 * m + 4 * lane);
+    const uint32_t u[2] = {v.x, v.y};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) y[m][e] = widen<DT>((uint16_t)(e & 1 ? u[e >> 1] >> 16 : u[e >> 1] & 0xffffu));
+  }
+  for (int j0 = w; j0 < ns; j0 += NW * U) {
+    uint2 xv[U][NM];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u * NW;
+      const int64_t row = j < ns ? (int64_t)crow[sv[j]] : 0;
+#pragma unroll
+      for (int m = 0; m < NM; ++m) xv[u][m] = *(const uint2*)(X + row * D + 256 * m + 4 * lane);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      double acc = 0.0;
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        const uint32_t uu[2] = {xv[u][m].x, xv[u][m].y};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc += (double)(widen<DT>((uint16_t)(e & 1 ? uu[e >> 1] >> 16 : uu[e >> 1] & 0xffffu)) * y[m][e]);
+      }
+#pragma unroll
+      for (int off = 32; off; off >>= 1) acc += __shfl_xor(acc, off);
+      const int j = j0 + u * NW;
+      if (lane == 0 && j < ns) sx[j] = acc;
+    }
+  }
+  __syncthreads();
+  // 5. top-k of the survivors by (exact score desc, row asc); NaN (cannot occur for live rows) last
+  for (int j = tid; j < ns; j += NT) {
+    const double sj = sx[j];
+    if (sj != sj) continue;
+    const int rj = crow[sv[j]];
+    int rank = 0;
+    for (int i = 0; i < ns; ++i) {
+      const double si = sx[i];
+      rank += si > sj || (si == sj && crow[sv[i]] < rj);
+    }
+    atomicAdd(&n_ok, 1);
+    if (rank < k) {
+      const float sf = (float)sj;
+      const long long rr = (long long)rj + row_offset;
+      if (out_rec)
+        out_rec[q * k + rank] = Rec{sf, 0, rr};
+      else {
+        out_s[q * k + rank] = sf;
+        out_r[q * k + rank] = rr;
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = n_ok + tid; i < k; i += NT) {
+    if (out_rec)
+      out_rec[q * k + i] = Rec{-__builtin_inff(), 0, -1};
+    else {
+      out_s[q * k + i] = -__builtin_inff();
+      out_r[q * k + i] = -1;
+    }
+  }
+  if (diag && tid == 0) {
+    diag[q * 2] = nc;
+    diag[q * 2 + 1] = ns;
+  }
+}
+
+}  // namespace
+
+// ---- host launchers --------------------------------------------------------------------------------
+bool screen_supported(int D, int dtype) { return (D == 768 || D == 1024) && (dtype == RFX_BF16 || dtype == RFX_F16); }
+
+void launch_screen_quantize(const void* X, int D, int dtype, int64_t tile0, int64_t ntiles, const int64_t* tiles_d,
+                            int8_t* codes, float* tscale, uint32_t* live, uint32_t* stats, hipStream_t st) {
+  if (ntiles <= 0) return;
+#define RFX_SQ(DTV, DV)                                                                                         \
+  hipLaunchKernelGGL((screen_quantize_kernel<DTV, DV>), dim3((unsigned)ntiles), dim3(256), 0, st, (const uint16_t*)X, \
+                     tile0, tiles_d, codes, tscale, live, stats)
+  if (dtype == RFX_BF16 && D == 768)
+    RFX_SQ(RFX_BF16, 768);
+  else if (dtype == RFX_BF16)
+    RFX_SQ(RFX_BF16, 1024);
+  else if (D == 768)
+    RFX_SQ(RFX_F16, 768);
+  else
+    RFX_SQ(RFX_F16, 1024);
+#undef RFX_SQ
+}
+
+MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k) {
+  MfmaPlan p{};
+  p.ok = screen_supported(D, dtype) && nrows > 0;
+  p.k_lane = k <= 4 ? 4 : (k <= 10 ? 10 : -1);
+  if (p.k_lane < 0) p.ok = false;
+  p.bn = k10::kQG;
+  p.q_blocks = (int)((nq + k10::kQG - 1) / k10::kQG);
+  p.nq_pad = (int64_t)p.q_blocks * k10::kQG;
+  if (p.q_blocks < 1 || p.q_blocks > 256) p.ok = false;
+  const int64_t ntiles = std::max<int64_t>((nrows + k10::kTM - 1) / k10::kTM, 1);
+  int64_t ranges = std::max<int64_t>(256 / std::max(p.q_blocks, 1), 1);
+  ranges = std::min<int64_t>(ranges, ntiles);
+  p.blocks = (int)ranges;
+  p.tiles_per_block = (int)((ntiles + ranges - 1) / ranges);
+  p.lists_per_block = 2;
+  p.n_lists = (int64_t)p.blocks * 2;
+  return p;
+}
+
+size_t tau_bytes_screen(const MfmaPlan& p) { return (size_t)p.nq_pad * k10::kTauW * sizeof(uint32_t); }
+
+void launch_screen_queries(const void* Q, int dtype, int D, int64_t nq, int64_t nq_pad, int8_t* Qc, float* qe2,
+                           const uint32_t* stats, uint32_t* tau, uint32_t* gate, hipStream_t st) {
+  const dim3 grid((unsigned)((nq_pad + 3) / 4));
+#define RFX_SQQ(DTV, DV)                                                                                       \
+  hipLaunchKernelGGL((screen_queries_kernel<DTV, DV>), grid, dim3(256), 0, st, (const uint16_t*)Q, (int)nq,      \
+                     (int)nq_pad, Qc, qe2, stats, tau, gate)
+  if (dtype == RFX_BF16 && D == 768)
+    RFX_SQQ(RFX_BF16, 768);
+  else if (dtype == RFX_BF16)
+    RFX_SQQ(RFX_BF16, 1024);
+  else if (D == 768)
+    RFX_SQQ(RFX_F16, 768);
+  else
+    RFX_SQQ(RFX_F16, 1024);
+#undef RFX_SQQ
+}
+
+int launch_scan_screen(const MfmaPlan& p, const int8_t* codes, const float* tscale, const uint32_t* live, int nrows,
+                       int D, const int8_t* Qc, const float* qe2, int nq, uint32_t* tau, float* cs, int* cr,
+                       uint32_t* drops, hipStream_t st, const uint32_t* mask) {
+  if (!p.ok || (D != 768 && D != 1024)) return -1;
+  const int ntiles = (nrows + k10::kTM - 1) / k10::kTM;
+  dim3 grid(p.blocks, p.q_blocks);
+  auto f = D == 768 ? k10::launch_768 : k10::launch_1024;
+  return f(p.k_lane, grid, st, codes, tscale, live, Qc, qe2, nq, ntiles, tau, cs, cr, drops, p.n_lists, mask);
+}
+
+int launch_screen_select(const float* cs, const int* cr, const uint32_t* drops, int64_t n_lists, int list_len,
+                         const float* qe2, const void* Q, const void* X, int D, int dtype, int64_t nq, int k,
+                         int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec, uint32_t* gate, int* diag,
+                         int force, hipStream_t st) {
+  if (nq <= 0) return 0;
+  if (k < 1 || k > 64) return -1;
+#define RFX_SEL(DTV, DV)                                                                                          \
+  hipLaunchKernelGGL((screen_select_kernel<DTV, DV>), dim3((unsigned)nq), dim3(512), 0, st, cs, cr, drops, n_lists, \
+                     list_len, qe2, (const uint16_t*)Q, (const uint16_t*)X, k, row_offset, out_s, out_r,           \
+                     (Rec*)out_rec, gate, diag, force)
+  if (dtype == RFX_BF16 && D == 768)
+    RFX_SEL(RFX_BF16, 768);
+  else if (dtype == RFX_BF16)
+    RFX_SEL(RFX_BF16, 1024);
+  else if (D == 768)
+    RFX_SEL(RFX_F16, 768);
+  else
+    RFX_SEL(RFX_F16, 1024);
+#undef RFX_SEL
+  return 0;
+}
+
+}  // namespace rfx

@@ -14,6 +14,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdlib>
@@ -68,8 +69,65 @@ struct Index {
   // launch); keyed by stream so concurrent searches on different streams never share it
   std::mutex state_mu;
   std::map<hipStream_t, uint32_t*> fused_state;
+  // int8 copy of the store for the exact two-pass scan (k_screen.hip): codes
+  // [scap][dim], per 32-row tile a scale and a live word, and stats[2] (max row norm, max
+  // quantisation-error norm, f32 bits).  screen: 0 off, 1 on, 2 on with every batch sent to the
+  // exact fallback (tests of the fallback path).
+  int screen = 0;
+  int64_t scap = 0;
+  int8_t* scodes = nullptr;
+  float* sscale = nullptr;
+  uint32_t* slive = nullptr;
+  uint32_t* sstats = nullptr;
   int64_t row_bytes() const { return (int64_t)dim * esize(dtype); }
 };
+
+void screen_free(Index& ix) {
+  for (void* p : {(void*)ix.scodes, (void*)ix.sscale, (void*)ix.slive, (void*)ix.sstats})
+    if (p) (void)hipFree(p);
+  ix.scodes = nullptr;
+  ix.sscale = nullptr;
+  ix.slive = nullptr;
+  ix.sstats = nullptr;
+  ix.scap = 0;
+}
+
+// (Re)build the whole int8 copy for the current capacity.
+int screen_build(Index& ix, hipStream_t st) {
+  screen_free(ix);
+  const int64_t cap = ix.capacity, nt = cap / 32;
+  if (cap == 0) return RFX_OK;
+  if (hipMalloc(&ix.scodes, (size_t)cap * ix.dim) != hipSuccess || hipMalloc(&ix.sscale, (size_t)nt * 4) != hipSuccess ||
+      hipMalloc(&ix.slive, (size_t)nt * 4) != hipSuccess || hipMalloc(&ix.sstats, 256) != hipSuccess) {
+    screen_free(ix);
+    return fail(RFX_ENOMEM, "hipMalloc failed for the int8 screen copy (%lld rows)", (long long)cap);
+  }
+  ix.scap = cap;
+  RFX_HIP(hipMemsetAsync(ix.scodes, 0, (size_t)cap * ix.dim, st));
+  RFX_HIP(hipMemsetAsync(ix.sscale, 0, (size_t)nt * 4, st));
+  RFX_HIP(hipMemsetAsync(ix.slive, 0, (size_t)nt * 4, st));
+  RFX_HIP(hipMemsetAsync(ix.sstats, 0, 256, st));
+  rfx::launch_screen_quantize(ix.data, ix.dim, ix.dtype, 0, (ix.rows + 31) / 32, nullptr, ix.scodes, ix.sscale, ix.slive,
+                              ix.sstats, st);
+  RFX_HIP(hipGetLastError());
+  RFX_HIP(hipStreamSynchronize(st));
+  return RFX_OK;
+}
+
+// Keep the int8 copy current after rows [first, rows) were written: re-quantise the tiles they
+// touch (the first one may have gained rows, so its scale can change); a grown buffer is rebuilt.
+int screen_update(Index& ix, int64_t first, hipStream_t st) {
+  if (!ix.screen) return RFX_OK;
+  if (ix.scap != ix.capacity) return screen_build(ix, st);
+  const int64_t t0 = first / 32, t1 = (ix.rows + 31) / 32;
+  if (t1 > t0) {
+    rfx::launch_screen_quantize(ix.data, ix.dim, ix.dtype, t0, t1 - t0, nullptr, ix.scodes, ix.sscale, ix.slive,
+                                ix.sstats, st);
+    RFX_HIP(hipGetLastError());
+    RFX_HIP(hipStreamSynchronize(st));
+  }
+  return RFX_OK;
+}
 
 int fused_state(Index& ix, hipStream_t st, uint32_t** out) {
   std::lock_guard<std::mutex> lk(ix.state_mu);
@@ -160,11 +218,22 @@ struct SearchLayout {
   rfx::MfmaPlan mp;
   int64_t n_cand;    // candidates per query
   size_t q_off, q_bytes, tau_off, cs_off, cr_off, total;
+  // kernel 10 (the two-pass scan): the exact plan above (kernel fbk, regions q/tau/cs/cr) is its
+  // gated fallback; the screen's own regions follow it
+  int fbk;
+  rfx::MfmaPlan sp;
+  size_t s_tau, s_cs, s_cr, s_drop, s_qc, s_qe2, s_gate, s_diag;
 };
 
 size_t align_up(size_t x) { return (x + 255) / 256 * 256; }
 
-int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
+int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L, bool search = false);
+
+// The search plan: the exact layout, extended by the two-pass scan's regions when the index holds an
+// int8 copy and the exact plan is the config-3 / config-4 kernel (6 / 8) it falls back to.
+int make_search_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) { return make_layout(ix, nq, k, L, true); }
+
+int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L, bool search) {
   if (k < 1 || k > 64) return fail(RFX_EINVAL, "k=%d out of range [1, 64]", k);
   if (nq < 0) return fail(RFX_EINVAL, "nq < 0");
   if (ix.rows >= (int64_t)INT32_MAX) return fail(RFX_EUNSUPPORTED, "shard exceeds 2^31-1 rows");
@@ -172,7 +241,8 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
   L.vp = rfx::plan_scan_valu(ix.rows, ix.dim, ix.dtype, nq, k);
   L.kernel = 0;
   if (nq > 8) {
-    if (nq > 128) {
+    // (with an int8 copy, 64 < nq <= 128 also plans kernel 6: it is the two-pass scan's fallback)
+    if (nq > 128 || (search && ix.screen && nq > 64)) {
       L.mp = rfx::plan_scan_mfma6(ix.rows, ix.dim, ix.dtype, nq, k);
       if (L.mp.ok) L.kernel = 6;
     }
@@ -242,6 +312,24 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) {
   L.cs_off = L.tau_off + align_up(tau_bytes);
   L.cr_off = L.cs_off + align_up((size_t)nq * L.n_cand * 4);
   L.total = L.cr_off + align_up((size_t)nq * L.n_cand * 4);
+  L.fbk = 0;
+  if (search && ix.screen && ix.rows > 0 && (L.kernel == 6 || L.kernel == 8)) {
+    L.sp = rfx::plan_scan_screen(ix.rows, ix.dim, ix.dtype, nq, k);
+    if (L.sp.ok) {
+      L.fbk = L.kernel;
+      L.kernel = 10;
+      const size_t nc = (size_t)L.sp.n_lists * L.sp.k_lane;
+      L.s_tau = L.total;
+      L.s_cs = L.s_tau + align_up(rfx::tau_bytes_screen(L.sp));
+      L.s_cr = L.s_cs + align_up((size_t)nq * nc * 4);
+      L.s_drop = L.s_cr + align_up((size_t)nq * nc * 4);
+      L.s_qc = L.s_drop + align_up((size_t)nq * L.sp.n_lists * 4);
+      L.s_qe2 = L.s_qc + align_up((size_t)L.sp.nq_pad * ix.dim);
+      L.s_gate = L.s_qe2 + align_up((size_t)L.sp.nq_pad * 4);
+      L.s_diag = L.s_gate + 256;
+      L.total = L.s_diag + align_up((size_t)nq * 8);
+    }
+  }
   return RFX_OK;
 }
 
@@ -336,6 +424,49 @@ int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq,
   return RFX_OK;
 }
 
+// The exact two-pass scan (kernel 10 + k_screen.hip): query codes, int8 screen,
+// select (survivors -> exact re-score -> top-k); then the exact scan + merge of the fallback plan,
+// gated on the device word the select kernel sets when a query's survivors may be incomplete.
+// Writes (out_s, out_r) or, with out_rec, the {score, pad, row + row_offset} records.
+int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t nq, int k, const uint32_t* mask,
+                  int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec, uint8_t* ws, hipStream_t st) {
+  if (nq == 0) return RFX_OK;
+  int8_t* qc = (int8_t*)(ws + L.s_qc);
+  float* qe2 = (float*)(ws + L.s_qe2);
+  uint32_t* stau = (uint32_t*)(ws + L.s_tau);
+  float* scs = (float*)(ws + L.s_cs);
+  int* scr = (int*)(ws + L.s_cr);
+  uint32_t* drops = (uint32_t*)(ws + L.s_drop);
+  uint32_t* gate = (uint32_t*)(ws + L.s_gate);
+  int* diag = (int*)(ws + L.s_diag);
+  rfx::launch_screen_queries(queries, ix.dtype, ix.dim, nq, L.sp.nq_pad, qc, qe2, ix.sstats, stau, gate, st);
+  if (rfx::launch_scan_screen(L.sp, ix.scodes, ix.sscale, ix.slive, (int)ix.rows, ix.dim, qc, qe2, (int)nq, stau, scs,
+                              scr, drops, st, mask) != 0)
+    return fail(RFX_EUNSUPPORTED, "screen scan launch rejected");
+  if (rfx::launch_screen_select(scs, scr, drops, L.sp.n_lists, L.sp.k_lane, qe2, queries, ix.data, ix.dim, ix.dtype, nq,
+                                k, row_offset, out_s, out_r, out_rec, gate, diag, ix.screen == 2, st) != 0)
+    return fail(RFX_EUNSUPPORTED, "screen select k=%d unsupported", k);
+  // gated exact pass (no work unless the select kernel set the gate)
+  const void* qpad = queries;
+  if (nq != L.mp.nq_pad || ((uintptr_t)queries & 15)) {
+    qpad = ws + L.q_off;
+    rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, 2, (void*)qpad, st);
+  }
+  uint32_t* tau = (uint32_t*)(ws + L.tau_off);
+  float* cs = (float*)(ws + L.cs_off);
+  int32_t* cr = (int32_t*)(ws + L.cr_off);
+  const int rc = L.fbk == 6 ? rfx::launch_scan_mfma6(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs,
+                                                     cr, st, mask, gate)
+                            : rfx::launch_scan_mfma8(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs,
+                                                     cr, st, mask, gate);
+  if (rc != 0) return fail(RFX_EUNSUPPORTED, "fallback scan launch rejected (%d)", rc);
+  if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.n_cand, L.mp.k_lane, k, row_offset, out_rec ? nullptr : out_s,
+                                   out_rec ? nullptr : out_r, out_rec, st, /*sorted=*/true, gate) != 0)
+    return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
 }  // namespace
 
 namespace rfx {
@@ -409,6 +540,7 @@ int rfx_index_destroy(rfx_index_t h) {
   }
   for (auto& kv : ix->fused_state) RFX_HIP(hipFree(kv.second));
   ix->fused_state.clear();
+  screen_free(*ix);
   return RFX_OK;
 }
 
@@ -429,7 +561,8 @@ int rfx_index_reserve(rfx_index_t h, int64_t capacity) {
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
   RFX_WLOCK(ix);
   RFX_HIP(hipSetDevice(ix->device));
-  return grow(*ix, capacity, nullptr);
+  const int rc = grow(*ix, capacity, nullptr);
+  return rc ? rc : screen_update(*ix, ix->rows, nullptr);
 }
 
 int rfx_index_add(rfx_index_t h, const void* vecs, int64_t n, int src_is_device, int64_t* out_first_row, void* stream) {
@@ -451,7 +584,7 @@ int rfx_index_add(rfx_index_t h, const void* vecs, int64_t n, int src_is_device,
   ix->live += n;
   ix->tomb.resize((size_t)(ix->rows + 7) / 8, 0);
   if (out_first_row) *out_first_row = first;
-  return RFX_OK;
+  return screen_update(*ix, first, st);
 }
 
 int rfx_index_add_synthetic(rfx_index_t h, uint64_t seed, int64_t gen_row0, int64_t n, int64_t* out_first_row,
@@ -474,7 +607,7 @@ int rfx_index_add_synthetic(rfx_index_t h, uint64_t seed, int64_t gen_row0, int6
   ix->live += n;
   ix->tomb.resize((size_t)(ix->rows + 7) / 8, 0);
   if (out_first_row) *out_first_row = first;
-  return RFX_OK;
+  return screen_update(*ix, first, st);
 }
 
 int rfx_index_tombstone(rfx_index_t h, const int64_t* rows_h, int64_t n, void* stream) {
@@ -504,6 +637,21 @@ int rfx_index_tombstone(rfx_index_t h, const int64_t* rows_h, int64_t n, void* s
   RFX_HIP(hipStreamSynchronize(st));
   RFX_HIP(hipFree(d));
   ix->live -= (int64_t)todo.size();
+  if (ix->screen) {  // the tombstoned rows' tiles: code 0, live bit clear, scale over the rest
+    if (ix->scap != ix->capacity) return screen_build(*ix, st);
+    std::vector<int64_t> tiles;
+    for (int64_t r : todo) tiles.push_back(r / 32);
+    std::sort(tiles.begin(), tiles.end());
+    tiles.erase(std::unique(tiles.begin(), tiles.end()), tiles.end());
+    int64_t* td = nullptr;
+    RFX_HIP(hipMalloc(&td, tiles.size() * sizeof(int64_t)));
+    RFX_HIP(hipMemcpyAsync(td, tiles.data(), tiles.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
+    rfx::launch_screen_quantize(ix->data, ix->dim, ix->dtype, 0, (int64_t)tiles.size(), td, ix->scodes, ix->sscale,
+                                ix->slive, ix->sstats, st);
+    RFX_HIP(hipGetLastError());
+    RFX_HIP(hipStreamSynchronize(st));
+    RFX_HIP(hipFree(td));
+  }
   return RFX_OK;
 }
 
@@ -711,11 +859,11 @@ int rfx_rows_sync(rfx_index_t h, const char* path, int64_t upto, int64_t file_ba
     fill_tail_nan(*ix, nullptr);
     return err;
   }
-  const int64_t n = upto - ix->rows;
+  const int64_t n = upto - ix->rows, first = ix->rows;
   ix->rows = upto;
   ix->live += n;
   ix->tomb.resize((size_t)(ix->rows + 7) / 8, 0);
-  return RFX_OK;
+  return screen_update(*ix, first, nullptr);
 }
 
 // ---- search ---------------------------------------------------------------------------------------
@@ -724,7 +872,7 @@ int rfx_search_workspace_bytes(rfx_index_t h, int64_t nq, int k, size_t* out_byt
   if (!ix || !out_bytes) return fail(RFX_EINVAL, "unknown index handle / null out");
   RFX_RLOCK(ix);
   SearchLayout L;
-  int rc = make_layout(*ix, nq, k, L);
+  int rc = make_search_layout(*ix, nq, k, L);  // >= every scan layout's workspace too
   if (rc) return rc;
   *out_bytes = L.total;
   return RFX_OK;
@@ -908,7 +1056,7 @@ int rfx_search_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k, c
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
   RFX_RLOCK(ix);
   SearchLayout L;
-  int rc = make_layout(*ix, nq, k, L);
+  int rc = make_search_layout(*ix, nq, k, L);
   if (rc) return rc;
   if (ws_bytes < L.total || (L.total && !ws_d)) return fail(RFX_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, L.total);
   if (nq > 0 && (!queries_d || !out_scores_d || !out_rows_d)) return fail(RFX_EINVAL, "null queries / outputs");
@@ -918,6 +1066,8 @@ int rfx_search_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k, c
   RFX_HIP(hipSetDevice(ix->device));
   hipStream_t st = (hipStream_t)stream;
   uint8_t* ws = (uint8_t*)ws_d;
+  if (L.kernel == 10)
+    return screen_search(*ix, L, queries_d, nq, k, row_mask_d, 0, out_scores_d, out_rows_d, nullptr, ws, st);
   float* cs = (float*)(ws + L.cs_off);
   int32_t* cr = (int32_t*)(ws + L.cr_off);
   // (the one-launch kernel reads the caller's queries with 16-B loads: an unaligned buffer takes
@@ -940,6 +1090,110 @@ int rfx_search_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k, c
                                    /*sorted=*/true) != 0)
     return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
   RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
+int rfx_search_records(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d,
+                       int64_t mask_words, int64_t row_offset, void* out_records_d, void* ws_d, size_t ws_bytes,
+                       void* stream) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  RFX_RLOCK(ix);
+  SearchLayout L;
+  int rc = make_search_layout(*ix, nq, k, L);
+  if (rc) return rc;
+  if (ws_bytes < L.total || (L.total && !ws_d)) return fail(RFX_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, L.total);
+  if (nq > 0 && (!queries_d || !out_records_d)) return fail(RFX_EINVAL, "null queries / output");
+  if (row_mask_d && mask_words < (ix->rows + 31) / 32)
+    return fail(RFX_EINVAL, "row mask has %lld words, the index needs %lld", (long long)mask_words,
+                (long long)((ix->rows + 31) / 32));
+  RFX_HIP(hipSetDevice(ix->device));
+  hipStream_t st = (hipStream_t)stream;
+  uint8_t* ws = (uint8_t*)ws_d;
+  if (L.kernel == 10)
+    return screen_search(*ix, L, queries_d, nq, k, row_mask_d, row_offset, nullptr, nullptr, out_records_d, ws, st);
+  if (nq == 0) return RFX_OK;
+  float* cs = (float*)(ws + L.cs_off);
+  int32_t* cr = (int32_t*)(ws + L.cr_off);
+  if (ix->rows == 0 || L.n_cand == 0) {  // an empty shard still contributes padding records
+    rc = rfx::launch_topk_merge_lists(cs, cr, 0, nq, 0, 1, k, row_offset, nullptr, nullptr, out_records_d, st);
+    if (rc != 0) return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
+    RFX_HIP(hipGetLastError());
+    return RFX_OK;
+  }
+  rc = scan_into(*ix, L, queries_d, nq, cs, cr, ws, st, row_mask_d);
+  if (rc) return rc;
+  const int list_len = L.kernel ? L.mp.k_lane : L.vp.k_slot;
+  if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.n_cand, list_len, k, row_offset, nullptr, nullptr, out_records_d, st,
+                                   /*sorted=*/true) != 0)
+    return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
+int rfx_search_plan(rfx_index_t h, int64_t nq, int k, int* out_kernel) {
+  auto ix = get(h);
+  if (!ix || !out_kernel) return fail(RFX_EINVAL, "unknown index handle / null out");
+  RFX_RLOCK(ix);
+  SearchLayout L;
+  int rc = make_search_layout(*ix, nq, k, L);
+  if (rc) return rc;
+  *out_kernel = L.kernel;
+  return RFX_OK;
+}
+
+// ---- the int8 screen copy (exact two-pass scan) ------------------------------------------------------
+int rfx_index_screen(rfx_index_t h, int mode, void* stream) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  if (mode < 0 || mode > 2) return fail(RFX_EINVAL, "screen mode %d (0 off, 1 on, 2 on + forced fallback)", mode);
+  if (mode && !rfx::screen_supported(ix->dim, ix->dtype))
+    return fail(RFX_EUNSUPPORTED, "the two-pass scan needs a bf16/f16 index of dim 768 or 1024 (dim=%d dtype=%d)",
+                ix->dim, ix->dtype);
+  hipStream_t st = (hipStream_t)stream;
+  RFX_WLOCK(ix);
+  RFX_HIP(hipSetDevice(ix->device));
+  if (!mode) {
+    RFX_HIP(hipDeviceSynchronize());  // no search still reads the copy
+    screen_free(*ix);
+    ix->screen = 0;
+    return RFX_OK;
+  }
+  const bool had = ix->screen != 0;
+  ix->screen = mode;
+  if (had && ix->scap == ix->capacity) return RFX_OK;
+  const int rc = screen_build(*ix, st);
+  if (rc) ix->screen = 0;
+  return rc;
+}
+
+int rfx_index_screen_read(rfx_index_t h, int64_t tile0, int64_t ntiles, int8_t* codes_h, float* scales_h,
+                          uint32_t* live_h, float* stats_h) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  RFX_RLOCK(ix);
+  if (!ix->screen) return fail(RFX_EINVAL, "the index holds no int8 screen copy");
+  if (tile0 < 0 || ntiles < 0 || (tile0 + ntiles) * 32 > ix->scap) return fail(RFX_EINVAL, "tiles out of range");
+  RFX_HIP(hipSetDevice(ix->device));
+  if (codes_h && ntiles)
+    RFX_HIP(hipMemcpy(codes_h, ix->scodes + tile0 * 32 * ix->dim, (size_t)ntiles * 32 * ix->dim, hipMemcpyDeviceToHost));
+  if (scales_h && ntiles) RFX_HIP(hipMemcpy(scales_h, ix->sscale + tile0, (size_t)ntiles * 4, hipMemcpyDeviceToHost));
+  if (live_h && ntiles) RFX_HIP(hipMemcpy(live_h, ix->slive + tile0, (size_t)ntiles * 4, hipMemcpyDeviceToHost));
+  if (stats_h) RFX_HIP(hipMemcpy(stats_h, ix->sstats, 8, hipMemcpyDeviceToHost));
+  return RFX_OK;
+}
+
+int rfx_screen_diag(rfx_index_t h, int64_t nq, int k, const void* ws_d, int32_t* diag_h, uint32_t* fallback_h) {
+  auto ix = get(h);
+  if (!ix || !ws_d) return fail(RFX_EINVAL, "unknown index handle / null workspace");
+  RFX_RLOCK(ix);
+  SearchLayout L;
+  int rc = make_search_layout(*ix, nq, k, L);
+  if (rc) return rc;
+  if (L.kernel != 10) return fail(RFX_EINVAL, "the search plan for nq=%lld k=%d is not the two-pass scan", (long long)nq, k);
+  RFX_HIP(hipSetDevice(ix->device));
+  if (diag_h && nq) RFX_HIP(hipMemcpy(diag_h, (const uint8_t*)ws_d + L.s_diag, (size_t)nq * 8, hipMemcpyDeviceToHost));
+  if (fallback_h) RFX_HIP(hipMemcpy(fallback_h, (const uint8_t*)ws_d + L.s_gate, 4, hipMemcpyDeviceToHost));
   return RFX_OK;
 }
 

@@ -81,8 +81,11 @@ int launch_scan_mfma5_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
                           uint32_t* tau, float* cs, int* cr, hipStream_t st);
 size_t tau_bytes_mfma6(const MfmaPlan& p);
 MfmaPlan plan_scan_mfma6(int64_t nrows, int D, int dtype, int64_t nq, int k);
+// gate (optional): a device word; the launch does nothing unless it is non-zero (the exact pass of
+// the two-pass scan runs only when the screen's select kernel asked for it)
 int launch_scan_mfma6(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr,
+                      const uint32_t* gate = nullptr);
 int launch_scan_mfma6_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, int dtype, const void* Qpad, int nq,
                           uint32_t* tau, float* cs, int* cr, hipStream_t st);
 size_t tau_bytes_mfma7(const MfmaPlan& p);
@@ -92,7 +95,8 @@ int launch_scan_mfma7(const MfmaPlan& p, const void* X, int nrows, int D, int dt
 size_t tau_bytes_mfma8(const MfmaPlan& p);
 MfmaPlan plan_scan_mfma8(int64_t nrows, int D, int dtype, int64_t nq, int k);
 int launch_scan_mfma8(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr,
+                      const uint32_t* gate = nullptr);
 // f32 stores (kernel 9): batched scan on v_mfma_f32_16x16x4_f32 for 16 < nq
 size_t tau_bytes_mfma9(const MfmaPlan& p);
 MfmaPlan plan_scan_mfma9(int64_t nrows, int D, int dtype, int64_t nq, int k);
@@ -107,9 +111,26 @@ int launch_topk_merge(const float* cs, const void* cr, int rows_are_i64, int64_t
 int launch_topk_merge_lists(const float* cs, const void* cr, int rows_are_i64, int64_t nq, int64_t n_cand,
                             int list_len, int k, int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec,
                             hipStream_t st,
-                            bool sorted = false);
+                            bool sorted = false, const uint32_t* gate = nullptr);
 int launch_merge_gathered(const void* rec, int world, int64_t nq, int k, float* out_s, int64_t* out_r,
                           hipStream_t st);
+
+// ---- the exact two-pass scan (kernel 10 + k_screen.hip) -----------------------------
+bool screen_supported(int D, int dtype);
+// int8 copy of tiles [tile0, tile0 + ntiles) (tiles_d == nullptr) or of the ntiles tiles listed in tiles_d
+void launch_screen_quantize(const void* X, int D, int dtype, int64_t tile0, int64_t ntiles, const int64_t* tiles_d,
+                            int8_t* codes, float* tscale, uint32_t* live, uint32_t* stats, hipStream_t st);
+MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k);
+size_t tau_bytes_screen(const MfmaPlan& p);
+void launch_screen_queries(const void* Q, int dtype, int D, int64_t nq, int64_t nq_pad, int8_t* Qc, float* qe2,
+                           const uint32_t* stats, uint32_t* tau, uint32_t* gate, hipStream_t st);
+int launch_scan_screen(const MfmaPlan& p, const int8_t* codes, const float* tscale, const uint32_t* live, int nrows,
+                       int D, const int8_t* Qc, const float* qe2, int nq, uint32_t* tau, float* cs, int* cr,
+                       uint32_t* drops, hipStream_t st, const uint32_t* mask);
+int launch_screen_select(const float* cs, const int* cr, const uint32_t* drops, int64_t n_lists, int list_len,
+                         const float* qe2, const void* Q, const void* X, int D, int dtype, int64_t nq, int k,
+                         int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec, uint32_t* gate, int* diag,
+                         int force, hipStream_t st);
 
 // ---- embedding ---------------------------------------------------------------------------------
 void launch_embed_weights(int V, int dim, uint64_t seed, void* wt, hipStream_t st);

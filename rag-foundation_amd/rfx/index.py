@@ -179,6 +179,61 @@ class DeviceIndex:
                                             ptr(ws), ws.numel(), stream_ptr(stream)))
         return out_s, out_r
 
+    def search_records(self, queries: torch.Tensor, k: int, row_offset: int = 0, out: torch.Tensor = None,
+                       workspace: torch.Tensor = None, stream=None, row_mask: torch.Tensor = None) -> torch.Tensor:
+        """The search as [nq][k][2] int64 merge records (score bits, row + row_offset): one shard's
+        all-gather input (rfx_search_records; the two-pass scan included)."""
+        q = self._check_queries(queries)
+        nq = q.shape[0]
+        if out is None:
+            out = torch.empty((nq, k, 2), dtype=torch.int64, device=q.device)
+        elif out.shape != (nq, k, 2) or out.dtype != torch.int64 or not out.is_contiguous():
+            raise ValueError(f"out must be a contiguous int64 [{nq}][{k}][2] tensor")
+        need = self.workspace_bytes(nq, k)
+        ws = workspace if workspace is not None and workspace.numel() >= need else \
+            torch.empty(max(need, 1), dtype=torch.uint8, device=q.device)
+        m, mw = self._check_mask(row_mask, q.device)
+        with torch.cuda.device(q.device):
+            check(lib.rfx_search_records(self.handle, ptr(q), nq, int(k), ptr(m) if m is not None else None, mw,
+                                         int(row_offset), ptr(out), ptr(ws), ws.numel(), stream_ptr(stream)))
+        return out
+
+    # ---- the exact two-pass scan (int8 copy of the store; DESIGN §4.10) --------------------------------
+    def enable_screen(self, mode: int = 1, stream=None) -> None:
+        """Keep an int8 copy of the rows (dim bytes per row) and answer batched searches with the
+        exact two-pass scan: int8 screen, exact re-score of the survivors, the exact scan as a gated
+        fallback.  mode 0 drops the copy; mode 2 forces the fallback (tests)."""
+        with torch.cuda.device(self.device):
+            check(lib.rfx_index_screen(self.handle, int(mode), stream_ptr(stream)))
+
+    def search_plan(self, nq: int, k: int) -> int:
+        """Kernel rfx_search runs for (nq, k): 10 = the two-pass scan."""
+        kern = ctypes.c_int()
+        check(lib.rfx_search_plan(self.handle, int(nq), int(k), ctypes.byref(kern)))
+        return kern.value
+
+    def screen_read(self, tile0: int, ntiles: int):
+        """(codes int8 [ntiles*32][dim], scales f32 [ntiles], live u32 [ntiles], stats f32 [2]) of the copy."""
+        import numpy as np
+        codes = np.empty((ntiles * 32, self.dim), dtype=np.int8)
+        scales = np.empty(ntiles, dtype=np.float32)
+        live = np.empty(ntiles, dtype=np.uint32)
+        stats = np.empty(2, dtype=np.float32)
+        with torch.cuda.device(self.device):
+            check(lib.rfx_index_screen_read(self.handle, int(tile0), int(ntiles), codes.ctypes.data, scales.ctypes.data,
+                                            live.ctypes.data, stats.ctypes.data))
+        return codes, scales, live, stats
+
+    def screen_diag(self, nq: int, k: int, workspace: torch.Tensor):
+        """After a two-pass search on `workspace`: (diag int32 [nq][2] = kept candidates, survivors
+        re-scored (-1: query sent to the fallback); fallback ran for the batch)."""
+        import numpy as np
+        diag = np.empty((nq, 2), dtype=np.int32)
+        fb = ctypes.c_uint32()
+        with torch.cuda.device(self.device):
+            check(lib.rfx_screen_diag(self.handle, int(nq), int(k), ptr(workspace), diag.ctypes.data, ctypes.byref(fb)))
+        return diag, bool(fb.value)
+
     def list_len(self, nq: int, k: int) -> int:
         """Length of the sorted candidate lists rfx_scan_topk writes (merge hint)."""
         n = ctypes.c_int()
