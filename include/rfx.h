@@ -185,7 +185,8 @@ int rfx_topk_merge_sorted(const float* cand_scores_d, const void* cand_rows_d, i
  * Costs dim bytes per row of extra HBM.  EUNSUPPORTED for f32 stores and other dims. */
 int rfx_index_screen(rfx_index_t h, int mode, void* stream);
 /* Inspection (tests): tiles [tile0, tile0 + ntiles) of the copy to host buffers (any may be NULL):
- * codes [ntiles*32][dim] int8, scales [ntiles] f32, live words [ntiles], stats [2] f32. */
+ * codes [ntiles*32][dim] int8, scales [ntiles] f32, live words [ntiles], stats [3] f32 (max row norm,
+ * max quantisation-error norm, max tile scale). */
 int rfx_index_screen_read(rfx_index_t h, int64_t tile0, int64_t ntiles, int8_t* codes_h, float* scales_h,
                           uint32_t* live_h, float* stats_h);
 /* The kernel rfx_search runs for (nq, k): 0 VALU, 1/2/3/6/8/9 exact MFMA scans, 10 the two-pass scan. */
@@ -200,6 +201,14 @@ int rfx_screen_diag(rfx_index_t h, int64_t nq, int k, const void* ws_d, int32_t*
 int rfx_search_records(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d,
                        int64_t mask_words, int64_t row_offset, void* out_records_d, void* ws_d, size_t ws_bytes,
                        void* stream);
+/* Benchmark / profiling form of the two above: writes (out_scores_d, out_rows_d) or, when
+ * out_records_d is not NULL, records; ev_scan_begin / ev_scan_end (hipEvent_t, may be NULL) are
+ * recorded on the stream right before and after the scan kernel (the int8 screen of the two-pass
+ * scan, the exact scan, or the one-launch VALU search as a whole). */
+int rfx_search_timed(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d,
+                     int64_t mask_words, int64_t row_offset, float* out_scores_d, int64_t* out_rows_d,
+                     void* out_records_d, void* ws_d, size_t ws_bytes, void* stream, void* ev_scan_begin,
+                     void* ev_scan_end);
 
 /* ---- RCCL communicators (SURVEY §8b rfx_init "RCCL comm if n>1", §8e) --------------------------
  * The all-gather of per-shard records runs on RCCL over xGMI from inside the library; the host

@@ -12,7 +12,8 @@ the rule keeps every row of the true top-k.
 Quantiser (per 32-row tile; dead rows = any NaN element: code 0, live bit clear):
     s_t = f32(amax over live rows) / 127 (IEEE f32 division; 0 when the tile has no live row)
     c   = clamp(rint(f32(x) / s_t), -127, 127)
-    stats = (max ||x||, max ||x - s_t c||) over live rows, rounded up to f32.
+    stats = (max ||x||, max ||x - s_t c||) over live rows, rounded up to f32, and max s_t (the
+            screen kernel's fast-path bound: no per-tile data on the fast path).
 Queries: s_y, c_y likewise per query; E_q = Xmax ||y - s_y c_y|| + Emax ||s_y c_y|| (Cauchy-Schwarz);
     e2 = (2 E_q + 4e-7 (Xmax + Emax) ||s_y c_y||) (1 + 1e-5) / s_y, rounded up to f32.
 Screen score (units of s_y): A = f32(c_x . c_y) * s_t (one f32 rounding).  Survivors of a query:
@@ -58,12 +59,14 @@ def quantize_tiles(rows32):
     xn = np.sqrt((np.where(dead[:, None], 0.0, xd) ** 2).sum(axis=1))
     en = np.sqrt((np.where(dead[:, None], 0.0, xd - rec) ** 2).sum(axis=1))
     stats = np.array([_f32_up(xn[~dead].max()) if (~dead).any() else 0.0,
-                      _f32_up(en[~dead].max()) if (~dead).any() else 0.0], dtype=np.float32)
+                      _f32_up(en[~dead].max()) if (~dead).any() else 0.0,
+                      s.max() if s.size else 0.0], dtype=np.float32)
     return c, s, live, stats
 
 
 def quantize_queries(q32, stats):
-    """q32 [nq][D] f32 (widened stored queries) -> (codes int8 [nq][D], e2 f32 [nq], s f32 [nq])."""
+    """q32 [nq][D] f32 (widened stored queries) -> (codes int8 [nq][D], e2 f32 [nq], s f32 [nq]);
+    stats as quantize_tiles returns them (the first two are used)."""
     y = np.asarray(q32, dtype=np.float32)
     amax = np.abs(y).max(axis=1).astype(np.float32)
     with np.errstate(divide="ignore", invalid="ignore"):

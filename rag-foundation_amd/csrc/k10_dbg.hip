@@ -1,0 +1,42 @@
+// k10_dbg.hip — DEBUG BUILD ONLY (librfx_dbg.so, `make dbg`): ablations and ring depths of the
+// two-pass scan's int8 screen (k_scan_screen.h MODE bits: 1 no top-k fold, 2 no launder, 4 prefetch
+// distance 1, 8 no corpus stream),
+// via rfx_dbg_screen_variant; variant = 100 * RING + MODE (RING in {4, 6, 8, 10, 12}).
+#include "k_scan_screen.h"
+
+namespace rfx {
+
+int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, const void* tmv, const uint32_t* sts,
+                           int nrows, const int8_t* Qc, const float* qe2, int nq, uint32_t* tau, float* cs, int* cr,
+                           uint32_t* dr, hipStream_t st) {
+  const uint4* tm = (const uint4*)tmv;
+  if (!p.ok || p.k_lane != 10) return -1;
+  const int ntiles = (nrows + k10::kTM - 1) / k10::kTM;
+  dim3 grid(p.blocks, p.q_blocks);
+#define RFX_K10V(R, M)                                                                                        \
+  case 100 * R + M:                                                                                          \
+    hipLaunchKernelGGL((k10::scan_screen_kernel<10, 768, false, R, M>), grid, dim3(512), 0, st, X, tm, sts, Qc, \
+                       qe2, nq, ntiles, tau, cs, cr, dr, p.n_lists, nullptr);                                \
+    break;
+  switch (variant) {
+    RFX_K10V(4, 0)
+    RFX_K10V(6, 0)
+    RFX_K10V(8, 0)
+    RFX_K10V(10, 0)
+    RFX_K10V(12, 0)
+    RFX_K10V(8, 1)
+    RFX_K10V(8, 8)
+    RFX_K10V(8, 9)
+    RFX_K10V(8, 2)
+    RFX_K10V(8, 4)
+    RFX_K10V(8, 32)
+    RFX_K10V(4, 2)
+    RFX_K10V(4, 4)
+    default:
+      return -1;
+  }
+#undef RFX_K10V
+  return 0;
+}
+
+}  // namespace rfx

@@ -45,6 +45,7 @@ int launch_scan_mfma6_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
     RFX_K6_DBG(256)
     RFX_K6_DBG(320)
     RFX_K6_DBG(512)
+    RFX_K6_DBG(1024)
 
     default:
       return -1;

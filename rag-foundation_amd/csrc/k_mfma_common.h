@@ -100,6 +100,21 @@ __device__ __forceinline__ void glds_sc1(const void* src, uint32_t lds_addr) {
                : "memory", "m0");
 }
 
+// Re-define registers through an empty asm.  Called on the resident query fragments right after the
+// explicit s_waitcnt vmcnt(0) that lands them: hipcc's wait-count pass cannot see the asm LDS-DMA
+// ops that share the vmcnt queue, so while it still tracks the fragments' loads it re-inserts
+// s_waitcnt vmcnt(N) before their first use in EVERY tile (merging the loop back-edge with the
+// preheader), and those waits drain the DMA ring (measured on kernel 10, round 3).
+template <int N>
+__device__ __forceinline__ void launder(uint4 (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    v4i32 t = __builtin_bit_cast(v4i32, v[i]);
+    asm volatile("" : "+v"(t));
+    v[i] = __builtin_bit_cast(uint4, t);
+  }
+}
+
 // 16 values of four 16x16 accumulators as one flat vector (no copies)
 struct Acc4View {
   const v4f32x4 (&a)[4];

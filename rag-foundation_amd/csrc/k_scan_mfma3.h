@@ -163,6 +163,13 @@ __global__ __launch_bounds__(256, 1) void scan_mfma3_kernel(const uint16_t* __re
   // the resident query loads must land before the LDS-DMA stream starts counting
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
+  for (int i = 0; i < NKS; ++i) {  // hipcc stops tracking the fragments' loads (mfc::launder, k_mfma_common.h)
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    v4i t = __builtin_bit_cast(v4i, bq[i]);
+    asm volatile("" : "+v"(t));
+    bq[i] = __builtin_bit_cast(uint4, t);
+  }
+#pragma unroll
   for (int p = 0; p < k3Ring; ++p) issue(p, p);
   asm volatile("s_waitcnt vmcnt(28)" ::: "memory");  // stage 0 landed (stages 1..7 in flight)
   asm volatile("s_barrier" ::: "memory");

@@ -252,6 +252,10 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
   static_assert((NST * KPS) % NF == 0, "fragment rotation must realign every tile");
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // resident queries landed before the counted stream
+  // NOT laundered (k_mfma_common.h): hipcc's own vmcnt waits on the fragments' loads stay in the loop
+  // and drain the DMA ring at the end of each tile's first stage — measured FASTER at the power cap
+  // (round 3, one box, interleaved bursts: 3.57 ms against 3.93 ms laundered, debug MODE 1024)
+  if constexpr ((MODE & 1024) != 0) launder(bq);
   issue_tau();
 #pragma unroll
   for (int p = 0; p < AHEAD; ++p)

@@ -184,6 +184,7 @@ __global__ __launch_bounds__(512, 1) void scan_mfma8_kernel(const uint16_t* __re
   float* const xw = (float*)(lds + kXOff);  // exchange: [wave][16][64] f32
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  launder(bq);  // hipcc stops tracking the fragments' loads (k_mfma_common.h)
   issue_tau();
 #pragma unroll
   for (int p = 0; p < AHEAD; ++p)

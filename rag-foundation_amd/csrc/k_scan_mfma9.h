@@ -178,6 +178,7 @@ __global__ __launch_bounds__(256, 1) void scan_mfma9_kernel(const float* __restr
   constexpr int YNG = (kRing - 2) * kGPW;  // ops younger than the next stage (8)
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  launder(bq);  // hipcc stops tracking the fragments' loads (k_mfma_common.h)
   issue_tau();
 #pragma unroll
   for (int p = 0; p < AHEAD; ++p)

@@ -31,7 +31,7 @@
 // 32-row tiles (block b takes tiles b, b + B, ...), a stage = 32 rows × 256 codes (8 KB) by LDS-DMA
 // into a RING-slot ring (one 1-KB piece per wave per stage), LDS image with chunk c of row r at
 // c ^ (r & 15), counted vmcnt + s_barrier per stage, v_permlane16_swap epilogue.
-// Algorithmic bytes per tile: 32 * D (codes) + 8 (tile scale, live word).
+// Algorithmic bytes per tile: 32 * D (codes) + 16 (the tile's metadata record).
 #pragma once
 #include "k_mfma_common.h"
 
@@ -55,8 +55,11 @@ constexpr int kGPW = 1;                   // LDS-DMA pieces per wave per stage (
 constexpr int kTauW = 16;                 // u32 per query in the threshold table (KL <= 10 used)
 constexpr int kTauBytes = kQG * kTauW * 4;  // 16 KB
 constexpr int kTauGPW = kTauBytes / 1024 / kWaves;
+constexpr int kMR = 8;  // tile-metadata slots (1 KB each: 64 lane copies of the 16-B record)
 template <int RING>
-constexpr int tau_off() { return RING * kSlot; }
+constexpr int meta_off() { return RING * kSlot; }
+template <int RING>
+constexpr int tau_off() { return meta_off<RING>() + kMR * 1024; }
 template <int RING>
 constexpr int list_off() { return tau_off<RING>() + kTauBytes; }
 template <int KL, int RING>
@@ -114,16 +117,23 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
   }
 }
 
-// X: int8 codes [ntiles * 32][D]; tscale / live: per tile; Qc: int8 query codes [nq_pad][D];
+// X: int8 codes [ntiles * 32][D]; tmeta: per tile {f32 scale, u32 live word, 0, 0}; stats: the
+// quantiser's maxima (stats[2] = max tile scale); Qc: int8 query codes [nq_pad][D];
 // qe2: [nq_pad] e2 per query (units of the query's scale).  Outputs per (query, list): KL
 // candidates (A, row) sorted best first, empty tail (-inf, kEmptyRow), and the list's drop.
-template <int KL, int D, bool MASK, int RING = kRing>
-__global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const float* __restrict__ tscale,
-                                                             const uint32_t* __restrict__ live, const int8_t* __restrict__ Qc,
-                                                             const float* __restrict__ qe2, int nq, int ntiles,
-                                                             uint32_t* __restrict__ tau, float* __restrict__ cand_s,
-                                                             int* __restrict__ cand_r, uint32_t* __restrict__ drops,
-                                                             int64_t n_lists, const uint32_t* __restrict__ mask) {
+// MODE: 0 production; debug-build ablations (k10_dbg.hip): 1 = no top-k fold (accumulators kept
+// live), 2 = resident fragments NOT laundered (hipcc's own vmcnt waits stay in the loop), 4 = A
+// fragments prefetched 2 k-steps ahead (d 768 only), 8 = no corpus stream after the prologue (MFMA +
+// LDS only; wrong scores, timing only), 32 = count slow-path entries (threshold slot 15 of each
+// wave's first query).
+template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
+__global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
+                                                             const uint32_t* __restrict__ stats,
+                                                             const int8_t* __restrict__ Qc, const float* __restrict__ qe2,
+                                                             int nq, int ntiles, uint32_t* __restrict__ tau,
+                                                             float* __restrict__ cand_s, int* __restrict__ cand_r,
+                                                             uint32_t* __restrict__ drops, int64_t n_lists,
+                                                             const uint32_t* __restrict__ mask) {
   constexpr int NKS = D / 64;    // 64-deep k-steps per tile
   constexpr int NST = D / kSK;   // stages per tile
   constexpr int KPS = kSK / 64;  // k-steps per stage (4)
@@ -131,6 +141,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   static_assert(KL <= 10, "threshold table holds 10 slots");
   __shared__ __attribute__((aligned(1024))) uint8_t lds[lds_bytes<KL, RING>()];
   constexpr int kTauOff = tau_off<RING>();
+  constexpr int kMetaOff = meta_off<RING>();
   constexpr int kListOff = list_off<RING>();
 
   const int tid = threadIdx.x;
@@ -145,6 +156,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   if (S == 0) return;
   const int lst = range * 2 + half;
   const float e2 = qe2[q];
+  const float smax = __uint_as_float(stats[2]);  // max tile scale of the store
 
   {
     uint4* tz = (uint4*)(lds + kTauOff);
@@ -173,13 +185,22 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   const uint32_t laneoff = (uint32_t)(pr * D + (((lane & 15) ^ (pr & 15)) * 16));
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
   const int64_t tile_stride = (int64_t)nblk * kTM * D;
+  // The tile metadata (scale, live word) rides the same counted stream: with the piece of a tile's
+  // first stage, every wave also DMAs the tile's 16-B record (64 lane copies, identical bytes from
+  // every wave) into meta slot (tile % kMR), read by the epilogue's slow path from LDS.
+  const v4i32 meta_rsrc = make_rsrc(tmeta);
   auto issue_piece = [&](int gi, int slot) {
+    const bool first = gi % NST == 0;  // (counted on the unclamped index: the waits stay exact)
     gi = gi < S ? gi : S - 1;  // tail: harmless duplicate loads keep the counted waits exact
     const int ti = gi / NST;
     const int si = gi - ti * NST;
     const int8_t* tbase = X + (int64_t)range * kTM * D + ti * tile_stride + si * kSK;
     const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)(slot * kSlot) + (uint32_t)(w * 1024));
     bdma_nt(make_rsrc(tbase), laneoff, dst);  // codes are read once per batch
+    if (first) {
+      const uint32_t mdst = __builtin_amdgcn_readfirstlane(lds_base + kMetaOff + (uint32_t)((ti % kMR) * 1024));
+      bdma(meta_rsrc, (uint32_t)(range + ti * nblk) * 16u, mdst);
+    }
   };
   const v4i32 tau_rsrc = make_rsrc(tau);
   auto issue_tau = [&]() {
@@ -192,6 +213,24 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   };
 
   uint32_t thr = 0u, drop = 0u;
+  // Fast-path bounds on the raw i32 dot D (no per-tile data): every tile scale s_t <= smax, so a
+  // lane value with D < ibound(thr) has fl(D s_t) < thr - e2 and is never looked at (proof in
+  // DESIGN §4.10).  ti_own: this lane's query (after the pair swap); ti_oth: the query the partner
+  // lane (lane ^ 16) owns, whose values this lane also holds before the swap.
+  auto ibound = [&](uint32_t t_o) -> int {
+    if (!t_o) return INT_MIN;
+    const float tf = unord(t_o) - e2;
+    if (!(tf > 0.f)) return INT_MIN;
+    if (!(smax > 0.f)) return INT_MAX;  // every A is 0 < tf
+    const float qv = __fdiv_rn(tf, smax) * 0.999999f;
+    return qv >= 2.0e9f ? INT_MAX : (int)floorf(qv);
+  };
+  int ti_own = INT_MIN, ti_oth = INT_MIN;
+  auto set_bounds = [&]() {
+    ti_own = ibound(thr);
+    ti_oth = __shfl_xor(ti_own, 16);
+  };
+  const bool odd = ((lane >> 4) & 1) != 0;
   const uint32_t slot_voff = (uint32_t)(q * kTauW + lst % KL) * 4u;
   const uint8_t* const tq = lds + kTauOff + (w * kQW + (lane & 15) + 16 * ((lane >> 4) & 1)) * (kTauW * 4);
   // A fragment of row block rb, k-step kk of a slot: row 16 rb + (lane & 15), chunk 4 kk + (lane >> 4)
@@ -211,31 +250,43 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   // Schedule: stage h's piece goes out at k-step 0 of stage h - (RING - 1) into the slot freed at
   // stage h - RING's barrier; fragments are read one k-step ahead; the stage-end wait + barrier sit
   // at k-step KPS - 1.
-  constexpr int PF = 1;
+  constexpr int PF = (D == 768 && (MODE & 4) == 0) ? 2 : 1;  // d 1024: 16 k-steps per tile, PF 2 would not realign
   constexpr int NF = PF + 1;
   constexpr int KB = KPS - PF;
   constexpr int AHEAD = RING - 1;
   constexpr int YNG = (RING - 2) * kGPW;  // ops younger than the next stage
   static_assert((NST * KPS) % NF == 0, "fragment rotation must realign every tile");
 
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // resident queries landed before the counted stream
+  if constexpr ((MODE & 2) == 0) launder(bq);
   issue_tau();
 #pragma unroll
   for (int p = 0; p < AHEAD; ++p) issue_piece(p, p);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(YNG) : "memory");
+  // stage 0 landed: younger are stages 1 .. AHEAD - 1 and the metadata records issued with stages
+  // 0 .. AHEAD - 1 (with piece 0's own record after it)
+  constexpr int NM0 = (AHEAD - 1) / NST + 1;
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(YNG + NM0) : "memory");
   asm volatile("s_barrier" ::: "memory");
 
   Frag fr[NF];
-  fr[0] = read_frag(0, 0);
+#pragma unroll
+  for (int p = 0; p < PF; ++p) fr[p] = read_frag(0, p);
   v4i32 acc4[4];  // [rb * 2 + qb]
   for (int it = 0; it < nt; ++it) {
     const int tile = range + it * nblk;
     const int gbase = it * NST;
-    // per-tile scale and live word: scalar loads, consumed in the epilogue
-    const float st = tscale[tile];
-    uint32_t lw = live[tile];
-    if constexpr (MASK) lw &= mask[tile];
-    if (it >= 2 && tau_refresh_tile(it - 2)) thr = max(thr, tau_min<KL>(tq));
+    if (it >= 2 && tau_refresh_tile(it - 2)) {
+      thr = max(thr, tau_min<KL>(tq));
+      set_bounds();
+    }
+    // metadata records younger than stage g+1's piece at stage s's wait: stages h in g+1 .. g+RING-1
+    // with h % NST == 0
+    auto nmeta = [&](int s) {
+      int c = 0;
+#pragma unroll
+      for (int j = 1; j <= RING - 1; ++j) c += (s + j) % NST == 0;
+      return c;
+    };
     auto young = [&](int s) {
       const int dmax = (RING - 3 + NST - s) / NST;
       bool y = false;
@@ -249,14 +300,30 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
       const int slot = g % RING;
 #pragma unroll
       for (int kk = 0; kk < KPS; ++kk) {
-        if (kk == 0) issue_piece(g + RING - 1, (g + RING - 1) % RING);
+        if constexpr ((MODE & 8) == 0)
+          if (kk == 0) issue_piece(g + RING - 1, (g + RING - 1) % RING);
         if (kk == KB) {
-          if (young(s))
-            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(YNG + kTauGPW) : "memory");
-          else
-            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(YNG) : "memory");
+          if constexpr ((MODE & 8) == 0) {
+            // younger than stage g+1's piece: stages g+2 .. g+RING-1 (YNG), the metadata records issued
+            // with stages g+1 .. g+RING-1 that start a tile (nmeta(s): s = g mod NST), a refresh
+            const int nm = nmeta(s) + (young(s) ? kTauGPW : 0);  // unrolled: a constant per stage
+            static_assert(kTauGPW == 2 && RING <= 13, "wait table below covers nm <= 6");
+            switch (nm) {
+#define RFX_K10_WAIT(N)                                                                  \
+  case N:                                                                                \
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(YNG + N) : "memory");            \
+    break;
+              RFX_K10_WAIT(0) RFX_K10_WAIT(1) RFX_K10_WAIT(2) RFX_K10_WAIT(3) RFX_K10_WAIT(4) RFX_K10_WAIT(5)
+              default:  // (nm <= 6 for RING <= 13, NST >= 3): stricter, never looser
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"(YNG + 6) : "memory");
+#undef RFX_K10_WAIT
+            }
+          } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          }
           asm volatile("s_barrier" ::: "memory");
-          if (s == NST - 1 && tau_refresh_tile(it)) issue_tau();
+          if constexpr ((MODE & 8) == 0)
+            if (s == NST - 1 && tau_refresh_tile(it)) issue_tau();
         }
         const int ks = s * KPS + kk;
         fr[(ks + PF) % NF] = kk + PF < KPS ? read_frag(slot, kk + PF) : read_frag((g + 1) % RING, kk + PF - KPS);
@@ -272,16 +339,41 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
       }
     }
 
-    // epilogue: pair swap (even 16-lane row keeps query n, odd keeps 16 + n), then fold
+    // epilogue.  Fast path: the max D of each of the lane's two queries against its integer bound
+    // (qb 0 values in acc4[0], acc4[2]; qb 1 in acc4[1], acc4[3]).  Only when some lane of the wave
+    // may hold a row to look at: the tile's scale and live word (LDS metadata slot), the pair swap (even
+    // 16-lane row keeps query n, odd keeps 16 + n) and the exact fold.
+    int m0 = max3i(acc4[0][0], acc4[0][1], acc4[0][2]);
+    int m1 = max3i(acc4[1][0], acc4[1][1], acc4[1][2]);
+    m0 = max3i(m0, acc4[0][3], acc4[2][0]);
+    m1 = max3i(m1, acc4[1][3], acc4[3][0]);
+    m0 = max3i(m0, acc4[2][1], acc4[2][2]);
+    m1 = max3i(m1, acc4[3][1], acc4[3][2]);
+    m0 = max(m0, acc4[2][3]);
+    m1 = max(m1, acc4[3][3]);
+    const bool hit = (odd ? m1 : m0) >= ti_own || (odd ? m0 : m1) >= ti_oth;
+    if constexpr ((MODE & 1) == 0) {
+      if (__builtin_amdgcn_ballot_w64(hit)) {
+        if constexpr ((MODE & 32) != 0)  // debug: count slow-path entries per wave (unused threshold slot 15)
+          if (lane == 0) atomicAdd(tau + (int64_t)(qg + w * kQW) * kTauW + 15, 1u);
+        const uint2 md = *(const uint2*)(lds + kMetaOff + (it % kMR) * 1024 + lane * 16);
+        const float st = __uint_as_float(md.x);
+        uint32_t lw = md.y;
+        if constexpr (MASK) lw &= mask[tile];
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+        for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const auto r = __builtin_amdgcn_permlane16_swap((uint32_t)acc4[2 * rb][i], (uint32_t)acc4[2 * rb + 1][i], false, false);
-        acc4[2 * rb][i] = (int)r[0];
-        acc4[2 * rb + 1][i] = (int)r[1];
+          for (int i = 0; i < 4; ++i) {
+            const auto r = __builtin_amdgcn_permlane16_swap((uint32_t)acc4[2 * rb][i], (uint32_t)acc4[2 * rb + 1][i], false, false);
+            acc4[2 * rb][i] = (int)r[0];
+            acc4[2 * rb + 1][i] = (int)r[1];
+          }
+        fold_screen<KL>(acc4, st, lw >> (8 * half), Ls, thr, e2, drop, tile * kTM + 8 * half, tau_rsrc, slot_voff);
+        set_bounds();
       }
-    fold_screen<KL>(acc4, st, lw >> (8 * half), Ls, thr, e2, drop, tile * kTM + 8 * half, tau_rsrc, slot_voff);
+    } else if (hit && m0 == 12345 && m1 == 54321) {
+      Ls[0] = 1;
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (q < nq) {
@@ -307,20 +399,20 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
 
 // one translation unit per D instantiates the kernel for KL in {4, 10}, with and without a filter mask
 #define RFX_K10_INSTANTIATE(DV, NAME)                                                                         \
-  int NAME(int kl, dim3 grid, hipStream_t st, const int8_t* X, const float* ts, const uint32_t* lv,           \
+  int NAME(int kl, dim3 grid, hipStream_t st, const int8_t* X, const uint4* tm, const uint32_t* sts,           \
            const int8_t* Qc, const float* qe2, int nq, int ntiles, uint32_t* tau, float* cs, int* cr,          \
            uint32_t* dr, int64_t n_lists, const uint32_t* mask) {                                            \
     if (kl == 4 && !mask)                                                                                   \
-      hipLaunchKernelGGL((scan_screen_kernel<4, DV, false>), grid, dim3(512), 0, st, X, ts, lv, Qc, qe2, nq,   \
+      hipLaunchKernelGGL((scan_screen_kernel<4, DV, false>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,   \
                          ntiles, tau, cs, cr, dr, n_lists, mask);                                            \
     else if (kl == 10 && !mask)                                                                             \
-      hipLaunchKernelGGL((scan_screen_kernel<10, DV, false>), grid, dim3(512), 0, st, X, ts, lv, Qc, qe2, nq,  \
+      hipLaunchKernelGGL((scan_screen_kernel<10, DV, false>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,  \
                          ntiles, tau, cs, cr, dr, n_lists, mask);                                            \
     else if (kl == 4)                                                                                       \
-      hipLaunchKernelGGL((scan_screen_kernel<4, DV, true>), grid, dim3(512), 0, st, X, ts, lv, Qc, qe2, nq,    \
+      hipLaunchKernelGGL((scan_screen_kernel<4, DV, true>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,    \
                          ntiles, tau, cs, cr, dr, n_lists, mask);                                            \
     else if (kl == 10)                                                                                      \
-      hipLaunchKernelGGL((scan_screen_kernel<10, DV, true>), grid, dim3(512), 0, st, X, ts, lv, Qc, qe2, nq,   \
+      hipLaunchKernelGGL((scan_screen_kernel<10, DV, true>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,   \
                          ntiles, tau, cs, cr, dr, n_lists, mask);                                            \
     else                                                                                                    \
       return -1;                                                                                            \

@@ -11,7 +11,7 @@
 namespace rfx {
 namespace k10 {
 #define RFX_K10_DECL(NAME)                                                                                    \
-  int NAME(int kl, dim3 grid, hipStream_t st, const int8_t* X, const float* ts, const uint32_t* lv,           \
+  int NAME(int kl, dim3 grid, hipStream_t st, const int8_t* X, const uint4* tm, const uint32_t* sts,           \
            const int8_t* Qc, const float* qe2, int nq, int ntiles, uint32_t* tau, float* cs, int* cr,          \
            uint32_t* dr, int64_t n_lists, const uint32_t* mask);
 RFX_K10_DECL(launch_768)
@@ -51,15 +51,17 @@ __device__ __forceinline__ int8_t code_of(float x, float s) {
 }
 
 // ---- the int8 copy: one 256-thread block per 32-row tile ----------------------------------------
+// Per tile a 16-B record {f32 scale, u32 live word (bit r = row r live), 0, 0}.
 // thread t: row t >> 3, segment t & 7 (D / 8 elements).  A row is dead (tombstone, NaN tail) when any
 // element is NaN: code 0, live bit clear, excluded from the scale.  s_t = amax / 127 over the live
 // rows (0 for a tile without any), c = clamp(rint(x / s_t), ±127).  stats[0] / stats[1] grow to the
-// max over live rows of ||x|| and ||x − s_t c|| (f64 sums, rounded up to f32, atomicMax on the bits).
+// max over live rows of ||x|| and ||x − s_t c|| (f64 sums, rounded up to f32, atomicMax on the bits),
+// stats[2] to the max tile scale.
 template <int DT, int D>
 __global__ __launch_bounds__(256) void screen_quantize_kernel(const uint16_t* __restrict__ X, int64_t tile0,
                                                               const int64_t* __restrict__ tiles,
-                                                              int8_t* __restrict__ codes, float* __restrict__ tscale,
-                                                              uint32_t* __restrict__ live, uint32_t* __restrict__ stats) {
+                                                              int8_t* __restrict__ codes, uint4* __restrict__ tmeta,
+                                                              uint32_t* __restrict__ stats) {
   constexpr int PER = D / 8;
   const int64_t tile = tiles ? tiles[blockIdx.x] : tile0 + blockIdx.x;
   const int t = threadIdx.x, row = t >> 3, seg = t & 7;
@@ -126,8 +128,8 @@ __global__ __launch_bounds__(256) void screen_quantize_kernel(const uint16_t* __
   }
   __syncthreads();
   if (t == 0) {
-    tscale[tile] = s;
-    live[tile] = word;
+    tmeta[tile] = uint4{__float_as_uint(s), word, 0u, 0u};  // kernel 10 DMAs this record per tile
+    atomicMax(stats + 2, __float_as_uint(s));              // the max tile scale (its fast-path bound)
   }
 }
 
@@ -355,11 +357,11 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
 bool screen_supported(int D, int dtype) { return (D == 768 || D == 1024) && (dtype == RFX_BF16 || dtype == RFX_F16); }
 
 void launch_screen_quantize(const void* X, int D, int dtype, int64_t tile0, int64_t ntiles, const int64_t* tiles_d,
-                            int8_t* codes, float* tscale, uint32_t* live, uint32_t* stats, hipStream_t st) {
+                            int8_t* codes, void* tmeta, uint32_t* stats, hipStream_t st) {
   if (ntiles <= 0) return;
 #define RFX_SQ(DTV, DV)                                                                                         \
   hipLaunchKernelGGL((screen_quantize_kernel<DTV, DV>), dim3((unsigned)ntiles), dim3(256), 0, st, (const uint16_t*)X, \
-                     tile0, tiles_d, codes, tscale, live, stats)
+                     tile0, tiles_d, codes, (uint4*)tmeta, stats)
   if (dtype == RFX_BF16 && D == 768)
     RFX_SQ(RFX_BF16, 768);
   else if (dtype == RFX_BF16)
@@ -409,14 +411,15 @@ void launch_screen_queries(const void* Q, int dtype, int D, int64_t nq, int64_t 
 #undef RFX_SQQ
 }
 
-int launch_scan_screen(const MfmaPlan& p, const int8_t* codes, const float* tscale, const uint32_t* live, int nrows,
-                       int D, const int8_t* Qc, const float* qe2, int nq, uint32_t* tau, float* cs, int* cr,
-                       uint32_t* drops, hipStream_t st, const uint32_t* mask) {
+int launch_scan_screen(const MfmaPlan& p, const int8_t* codes, const void* tmeta, const uint32_t* stats, int nrows, int D,
+                       const int8_t* Qc, const float* qe2, int nq, uint32_t* tau, float* cs, int* cr, uint32_t* drops,
+                       hipStream_t st, const uint32_t* mask) {
   if (!p.ok || (D != 768 && D != 1024)) return -1;
   const int ntiles = (nrows + k10::kTM - 1) / k10::kTM;
   dim3 grid(p.blocks, p.q_blocks);
   auto f = D == 768 ? k10::launch_768 : k10::launch_1024;
-  return f(p.k_lane, grid, st, codes, tscale, live, Qc, qe2, nq, ntiles, tau, cs, cr, drops, p.n_lists, mask);
+  return f(p.k_lane, grid, st, codes, (const uint4*)tmeta, stats, Qc, qe2, nq, ntiles, tau, cs, cr, drops, p.n_lists,
+           mask);
 }
 
 int launch_screen_select(const float* cs, const int* cr, const uint32_t* drops, int64_t n_lists, int list_len,

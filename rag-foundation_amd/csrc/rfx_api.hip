@@ -70,24 +70,22 @@ struct Index {
   std::mutex state_mu;
   std::map<hipStream_t, uint32_t*> fused_state;
   // int8 copy of the store for the exact two-pass scan (k_screen.hip): codes
-  // [scap][dim], per 32-row tile a scale and a live word, and stats[2] (max row norm, max
-  // quantisation-error norm, f32 bits).  screen: 0 off, 1 on, 2 on with every batch sent to the
+  // [scap][dim], per 32-row tile a 16-B record (scale, live word), and stats[3] (max row norm, max
+  // quantisation-error norm, max tile scale; f32 bits).  screen: 0 off, 1 on, 2 on with every batch sent to the
   // exact fallback (tests of the fallback path).
   int screen = 0;
   int64_t scap = 0;
   int8_t* scodes = nullptr;
-  float* sscale = nullptr;
-  uint32_t* slive = nullptr;
+  void* smeta = nullptr;  // per tile {f32 scale, u32 live word, 0, 0}
   uint32_t* sstats = nullptr;
   int64_t row_bytes() const { return (int64_t)dim * esize(dtype); }
 };
 
 void screen_free(Index& ix) {
-  for (void* p : {(void*)ix.scodes, (void*)ix.sscale, (void*)ix.slive, (void*)ix.sstats})
+  for (void* p : {(void*)ix.scodes, ix.smeta, (void*)ix.sstats})
     if (p) (void)hipFree(p);
   ix.scodes = nullptr;
-  ix.sscale = nullptr;
-  ix.slive = nullptr;
+  ix.smeta = nullptr;
   ix.sstats = nullptr;
   ix.scap = 0;
 }
@@ -97,18 +95,16 @@ int screen_build(Index& ix, hipStream_t st) {
   screen_free(ix);
   const int64_t cap = ix.capacity, nt = cap / 32;
   if (cap == 0) return RFX_OK;
-  if (hipMalloc(&ix.scodes, (size_t)cap * ix.dim) != hipSuccess || hipMalloc(&ix.sscale, (size_t)nt * 4) != hipSuccess ||
-      hipMalloc(&ix.slive, (size_t)nt * 4) != hipSuccess || hipMalloc(&ix.sstats, 256) != hipSuccess) {
+  if (hipMalloc(&ix.scodes, (size_t)cap * ix.dim) != hipSuccess || hipMalloc(&ix.smeta, (size_t)nt * 16) != hipSuccess ||
+      hipMalloc(&ix.sstats, 256) != hipSuccess) {
     screen_free(ix);
     return fail(RFX_ENOMEM, "hipMalloc failed for the int8 screen copy (%lld rows)", (long long)cap);
   }
   ix.scap = cap;
   RFX_HIP(hipMemsetAsync(ix.scodes, 0, (size_t)cap * ix.dim, st));
-  RFX_HIP(hipMemsetAsync(ix.sscale, 0, (size_t)nt * 4, st));
-  RFX_HIP(hipMemsetAsync(ix.slive, 0, (size_t)nt * 4, st));
+  RFX_HIP(hipMemsetAsync(ix.smeta, 0, (size_t)nt * 16, st));
   RFX_HIP(hipMemsetAsync(ix.sstats, 0, 256, st));
-  rfx::launch_screen_quantize(ix.data, ix.dim, ix.dtype, 0, (ix.rows + 31) / 32, nullptr, ix.scodes, ix.sscale, ix.slive,
-                              ix.sstats, st);
+  rfx::launch_screen_quantize(ix.data, ix.dim, ix.dtype, 0, (ix.rows + 31) / 32, nullptr, ix.scodes, ix.smeta, ix.sstats, st);
   RFX_HIP(hipGetLastError());
   RFX_HIP(hipStreamSynchronize(st));
   return RFX_OK;
@@ -121,8 +117,7 @@ int screen_update(Index& ix, int64_t first, hipStream_t st) {
   if (ix.scap != ix.capacity) return screen_build(ix, st);
   const int64_t t0 = first / 32, t1 = (ix.rows + 31) / 32;
   if (t1 > t0) {
-    rfx::launch_screen_quantize(ix.data, ix.dim, ix.dtype, t0, t1 - t0, nullptr, ix.scodes, ix.sscale, ix.slive,
-                                ix.sstats, st);
+    rfx::launch_screen_quantize(ix.data, ix.dim, ix.dtype, t0, t1 - t0, nullptr, ix.scodes, ix.smeta, ix.sstats, st);
     RFX_HIP(hipGetLastError());
     RFX_HIP(hipStreamSynchronize(st));
   }
@@ -429,7 +424,8 @@ int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq,
 // gated on the device word the select kernel sets when a query's survivors may be incomplete.
 // Writes (out_s, out_r) or, with out_rec, the {score, pad, row + row_offset} records.
 int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t nq, int k, const uint32_t* mask,
-                  int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec, uint8_t* ws, hipStream_t st) {
+                  int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec, uint8_t* ws, hipStream_t st,
+                  void* ev0 = nullptr, void* ev1 = nullptr) {
   if (nq == 0) return RFX_OK;
   int8_t* qc = (int8_t*)(ws + L.s_qc);
   float* qe2 = (float*)(ws + L.s_qe2);
@@ -440,9 +436,11 @@ int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t
   uint32_t* gate = (uint32_t*)(ws + L.s_gate);
   int* diag = (int*)(ws + L.s_diag);
   rfx::launch_screen_queries(queries, ix.dtype, ix.dim, nq, L.sp.nq_pad, qc, qe2, ix.sstats, stau, gate, st);
-  if (rfx::launch_scan_screen(L.sp, ix.scodes, ix.sscale, ix.slive, (int)ix.rows, ix.dim, qc, qe2, (int)nq, stau, scs,
+  if (ev0) RFX_HIP(hipEventRecord((hipEvent_t)ev0, st));
+  if (rfx::launch_scan_screen(L.sp, ix.scodes, ix.smeta, ix.sstats, (int)ix.rows, ix.dim, qc, qe2, (int)nq, stau, scs,
                               scr, drops, st, mask) != 0)
     return fail(RFX_EUNSUPPORTED, "screen scan launch rejected");
+  if (ev1) RFX_HIP(hipEventRecord((hipEvent_t)ev1, st));
   if (rfx::launch_screen_select(scs, scr, drops, L.sp.n_lists, L.sp.k_lane, qe2, queries, ix.data, ix.dim, ix.dtype, nq,
                                 k, row_offset, out_s, out_r, out_rec, gate, diag, ix.screen == 2, st) != 0)
     return fail(RFX_EUNSUPPORTED, "screen select k=%d unsupported", k);
@@ -646,8 +644,8 @@ int rfx_index_tombstone(rfx_index_t h, const int64_t* rows_h, int64_t n, void* s
     int64_t* td = nullptr;
     RFX_HIP(hipMalloc(&td, tiles.size() * sizeof(int64_t)));
     RFX_HIP(hipMemcpyAsync(td, tiles.data(), tiles.size() * sizeof(int64_t), hipMemcpyHostToDevice, st));
-    rfx::launch_screen_quantize(ix->data, ix->dim, ix->dtype, 0, (int64_t)tiles.size(), td, ix->scodes, ix->sscale,
-                                ix->slive, ix->sstats, st);
+    rfx::launch_screen_quantize(ix->data, ix->dim, ix->dtype, 0, (int64_t)tiles.size(), td, ix->scodes, ix->smeta,
+                                ix->sstats, st);
     RFX_HIP(hipGetLastError());
     RFX_HIP(hipStreamSynchronize(st));
     RFX_HIP(hipFree(td));
@@ -1032,6 +1030,61 @@ int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k
   return RFX_OK;
 }
 
+}  // extern "C"
+namespace rfx {
+constexpr int k10_tau_words() { return 16; }  // k_scan_screen.h kTauW
+int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, const void* tmv, const uint32_t* sts,
+                           int nrows, const int8_t* Qc, const float* qe2, int nq, uint32_t* tau, float* cs, int* cr,
+                           uint32_t* dr, hipStream_t st);
+}
+extern "C" {
+// Diagnostic (k10_dbg.hip): the two-pass scan's query quantiser + one kernel-10 variant
+// (100 * RING + MODE), or variant 9: a plain streaming read of the int8 copy (its HBM ceiling).
+int rfx_dbg_screen_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k, int variant, void* ws_d,
+                           size_t ws_bytes, void* stream) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  RFX_RLOCK(ix);
+  SearchLayout L;
+  int rc = make_search_layout(*ix, nq, k, L);
+  if (rc) return rc;
+  if (L.kernel != 10 || ws_bytes < L.total) return fail(RFX_EINVAL, "variant needs a two-pass plan and its workspace");
+  hipStream_t st = (hipStream_t)stream;
+  uint8_t* ws = (uint8_t*)ws_d;
+  if (variant == 9) {
+    rfx::launch_stream_read(ix->scodes, ix->rows * ix->dim, (uint32_t*)(ws + L.s_gate), st);
+    RFX_HIP(hipGetLastError());
+    return RFX_OK;
+  }
+  int8_t* qc = (int8_t*)(ws + L.s_qc);
+  float* qe2 = (float*)(ws + L.s_qe2);
+  uint32_t* stau = (uint32_t*)(ws + L.s_tau);
+  rfx::launch_screen_queries(queries_d, ix->dtype, ix->dim, nq, L.sp.nq_pad, qc, qe2, ix->sstats, stau,
+                             (uint32_t*)(ws + L.s_gate), st);
+  if (rfx::launch_scan_screen_dbg(L.sp, variant, ix->scodes, ix->smeta, ix->sstats, (int)ix->rows, qc, qe2, (int)nq, stau,
+                                  (float*)(ws + L.s_cs), (int*)(ws + L.s_cr), (uint32_t*)(ws + L.s_drop), st) != 0)
+    return fail(RFX_EUNSUPPORTED, "screen variant %d unsupported", variant);
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
+// Diagnostic: after a kernel-10 variant with MODE 32, the slow-path entries it counted (sum over waves).
+int rfx_dbg_screen_counts(rfx_index_t h, int64_t nq, int k, const void* ws_d, uint64_t* out) {
+  auto ix = get(h);
+  if (!ix || !out) return fail(RFX_EINVAL, "unknown index handle / null out");
+  RFX_RLOCK(ix);
+  SearchLayout L;
+  int rc = make_search_layout(*ix, nq, k, L);
+  if (rc) return rc;
+  if (L.kernel != 10) return fail(RFX_EINVAL, "not a two-pass plan");
+  std::vector<uint32_t> t((size_t)L.sp.nq_pad * rfx::k10_tau_words());
+  RFX_HIP(hipMemcpy(t.data(), (const uint8_t*)ws_d + L.s_tau, t.size() * 4, hipMemcpyDeviceToHost));
+  uint64_t n = 0;
+  for (size_t q = 0; q < (size_t)L.sp.nq_pad; ++q) n += t[q * rfx::k10_tau_words() + 15];
+  *out = n;
+  return RFX_OK;
+}
+
 // Diagnostic: read the whole index once with a plain dwordx4 streaming kernel (HBM ceiling).
 int rfx_dbg_stream_read(rfx_index_t h, void* scratch4_d, void* stream) {
   auto ix = get(h);
@@ -1049,9 +1102,16 @@ int rfx_search(rfx_index_t h, const void* queries_d, int64_t nq, int k, float* o
   return rfx_search_masked(h, queries_d, nq, k, nullptr, 0, out_scores_d, out_rows_d, ws_d, ws_bytes, stream);
 }
 
-int rfx_search_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d,
-                      int64_t mask_words, float* out_scores_d, int64_t* out_rows_d, void* ws_d, size_t ws_bytes,
-                      void* stream) {
+}  // extern "C"
+
+namespace {
+// One search (every rfx_search* entry point): writes (out_s, out_r) or, with out_rec, merge
+// records with row_offset added.  ev0 / ev1 (hipEvent_t, optional) are recorded on the stream
+// right before and after the scan kernel (the two-pass scan's int8 screen; the exact scan; the
+// one-launch VALU search as a whole): the benchmark's per-kernel timing.
+int search_impl(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d, int64_t mask_words,
+                int64_t row_offset, float* out_scores_d, int64_t* out_rows_d, void* out_rec, void* ws_d, size_t ws_bytes,
+                void* stream, void* ev0, void* ev1) {
   auto ix = get(h);
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
   RFX_RLOCK(ix);
@@ -1059,76 +1119,79 @@ int rfx_search_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k, c
   int rc = make_search_layout(*ix, nq, k, L);
   if (rc) return rc;
   if (ws_bytes < L.total || (L.total && !ws_d)) return fail(RFX_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, L.total);
-  if (nq > 0 && (!queries_d || !out_scores_d || !out_rows_d)) return fail(RFX_EINVAL, "null queries / outputs");
+  if (nq > 0 && (!queries_d || (!out_rec && (!out_scores_d || !out_rows_d)))) return fail(RFX_EINVAL, "null queries / outputs");
   if (row_mask_d && mask_words < (ix->rows + 31) / 32)
     return fail(RFX_EINVAL, "row mask has %lld words, the index needs %lld", (long long)mask_words,
                 (long long)((ix->rows + 31) / 32));
   RFX_HIP(hipSetDevice(ix->device));
   hipStream_t st = (hipStream_t)stream;
   uint8_t* ws = (uint8_t*)ws_d;
+  auto mark = [&](void* ev) -> int {
+    if (ev) RFX_HIP(hipEventRecord((hipEvent_t)ev, st));
+    return RFX_OK;
+  };
   if (L.kernel == 10)
-    return screen_search(*ix, L, queries_d, nq, k, row_mask_d, 0, out_scores_d, out_rows_d, nullptr, ws, st);
+    return screen_search(*ix, L, queries_d, nq, k, row_mask_d, row_offset, out_scores_d, out_rows_d, out_rec, ws, st,
+                         ev0, ev1);
+  if (nq == 0) return RFX_OK;
   float* cs = (float*)(ws + L.cs_off);
   int32_t* cr = (int32_t*)(ws + L.cr_off);
   // (the one-launch kernel reads the caller's queries with 16-B loads: an unaligned buffer takes
   // the three-launch path, whose widening copy is aligned)
-  if (L.kernel == 0 && ix->rows > 0 && nq > 0 && nq <= rfx::kValuFusedMaxNq && fused_enabled() &&
+  if (!out_rec && row_offset == 0 && L.kernel == 0 && ix->rows > 0 && nq <= rfx::kValuFusedMaxNq && fused_enabled() &&
       ((uintptr_t)queries_d & 15) == 0) {
     uint32_t* state = nullptr;
     if ((rc = fused_state(*ix, st, &state))) return rc;
+    if ((rc = mark(ev0))) return rc;
     if (rfx::launch_search_valu_fused(L.vp, ix->data, (int)ix->rows, ix->dim, ix->dtype, queries_d, (int)nq, cs, cr,
                                       state, k, out_scores_d, out_rows_d, st, row_mask_d) != 0)
       return fail(RFX_EUNSUPPORTED, "VALU search launch rejected");
     RFX_HIP(hipGetLastError());
-    return RFX_OK;
+    return mark(ev1);
   }
-  rc = scan_into(*ix, L, queries_d, nq, cs, cr, ws, st, row_mask_d);
-  if (rc) return rc;
+  int64_t n_cand = L.n_cand;
+  int list_len = L.kernel ? L.mp.k_lane : L.vp.k_slot;
+  if (ix->rows == 0 || n_cand == 0) {  // an empty index: padding only
+    n_cand = 0;
+    list_len = 1;
+  } else {
+    if ((rc = mark(ev0))) return rc;
+    rc = scan_into(*ix, L, queries_d, nq, cs, cr, ws, st, row_mask_d);
+    if (rc) return rc;
+    if ((rc = mark(ev1))) return rc;
+  }
   // the scan's candidates are sorted lists: the merge bounds admission by the lists' k-th entries
-  const int list_len = L.kernel ? L.mp.k_lane : L.vp.k_slot;
-  if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.n_cand, list_len, k, 0, out_scores_d, out_rows_d, nullptr, st,
-                                   /*sorted=*/true) != 0)
+  if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, n_cand, list_len, k, row_offset, out_rec ? nullptr : out_scores_d,
+                                   out_rec ? nullptr : out_rows_d, out_rec, st, /*sorted=*/n_cand > 0) != 0)
     return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
   RFX_HIP(hipGetLastError());
   return RFX_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int rfx_search_masked(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d,
+                      int64_t mask_words, float* out_scores_d, int64_t* out_rows_d, void* ws_d, size_t ws_bytes,
+                      void* stream) {
+  return search_impl(h, queries_d, nq, k, row_mask_d, mask_words, 0, out_scores_d, out_rows_d, nullptr, ws_d, ws_bytes,
+                     stream, nullptr, nullptr);
 }
 
 int rfx_search_records(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d,
                        int64_t mask_words, int64_t row_offset, void* out_records_d, void* ws_d, size_t ws_bytes,
                        void* stream) {
-  auto ix = get(h);
-  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
-  RFX_RLOCK(ix);
-  SearchLayout L;
-  int rc = make_search_layout(*ix, nq, k, L);
-  if (rc) return rc;
-  if (ws_bytes < L.total || (L.total && !ws_d)) return fail(RFX_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, L.total);
-  if (nq > 0 && (!queries_d || !out_records_d)) return fail(RFX_EINVAL, "null queries / output");
-  if (row_mask_d && mask_words < (ix->rows + 31) / 32)
-    return fail(RFX_EINVAL, "row mask has %lld words, the index needs %lld", (long long)mask_words,
-                (long long)((ix->rows + 31) / 32));
-  RFX_HIP(hipSetDevice(ix->device));
-  hipStream_t st = (hipStream_t)stream;
-  uint8_t* ws = (uint8_t*)ws_d;
-  if (L.kernel == 10)
-    return screen_search(*ix, L, queries_d, nq, k, row_mask_d, row_offset, nullptr, nullptr, out_records_d, ws, st);
-  if (nq == 0) return RFX_OK;
-  float* cs = (float*)(ws + L.cs_off);
-  int32_t* cr = (int32_t*)(ws + L.cr_off);
-  if (ix->rows == 0 || L.n_cand == 0) {  // an empty shard still contributes padding records
-    rc = rfx::launch_topk_merge_lists(cs, cr, 0, nq, 0, 1, k, row_offset, nullptr, nullptr, out_records_d, st);
-    if (rc != 0) return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
-    RFX_HIP(hipGetLastError());
-    return RFX_OK;
-  }
-  rc = scan_into(*ix, L, queries_d, nq, cs, cr, ws, st, row_mask_d);
-  if (rc) return rc;
-  const int list_len = L.kernel ? L.mp.k_lane : L.vp.k_slot;
-  if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.n_cand, list_len, k, row_offset, nullptr, nullptr, out_records_d, st,
-                                   /*sorted=*/true) != 0)
-    return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
-  RFX_HIP(hipGetLastError());
-  return RFX_OK;
+  if (nq > 0 && !out_records_d) return fail(RFX_EINVAL, "null output");
+  return search_impl(h, queries_d, nq, k, row_mask_d, mask_words, row_offset, nullptr, nullptr, out_records_d, ws_d,
+                     ws_bytes, stream, nullptr, nullptr);
+}
+
+int rfx_search_timed(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d,
+                     int64_t mask_words, int64_t row_offset, float* out_scores_d, int64_t* out_rows_d,
+                     void* out_records_d, void* ws_d, size_t ws_bytes, void* stream, void* ev_scan_begin,
+                     void* ev_scan_end) {
+  return search_impl(h, queries_d, nq, k, row_mask_d, mask_words, row_offset, out_scores_d, out_rows_d, out_records_d,
+                     ws_d, ws_bytes, stream, ev_scan_begin, ev_scan_end);
 }
 
 int rfx_search_plan(rfx_index_t h, int64_t nq, int k, int* out_kernel) {
@@ -1177,9 +1240,15 @@ int rfx_index_screen_read(rfx_index_t h, int64_t tile0, int64_t ntiles, int8_t* 
   RFX_HIP(hipSetDevice(ix->device));
   if (codes_h && ntiles)
     RFX_HIP(hipMemcpy(codes_h, ix->scodes + tile0 * 32 * ix->dim, (size_t)ntiles * 32 * ix->dim, hipMemcpyDeviceToHost));
-  if (scales_h && ntiles) RFX_HIP(hipMemcpy(scales_h, ix->sscale + tile0, (size_t)ntiles * 4, hipMemcpyDeviceToHost));
-  if (live_h && ntiles) RFX_HIP(hipMemcpy(live_h, ix->slive + tile0, (size_t)ntiles * 4, hipMemcpyDeviceToHost));
-  if (stats_h) RFX_HIP(hipMemcpy(stats_h, ix->sstats, 8, hipMemcpyDeviceToHost));
+  if ((scales_h || live_h) && ntiles) {
+    std::vector<uint32_t> m((size_t)ntiles * 4);
+    RFX_HIP(hipMemcpy(m.data(), (const uint8_t*)ix->smeta + tile0 * 16, m.size() * 4, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < ntiles; ++i) {
+      if (scales_h) memcpy(scales_h + i, &m[4 * i], 4);
+      if (live_h) live_h[i] = m[4 * i + 1];
+    }
+  }
+  if (stats_h) RFX_HIP(hipMemcpy(stats_h, ix->sstats, 12, hipMemcpyDeviceToHost));
   return RFX_OK;
 }
 

@@ -118,15 +118,16 @@ int launch_merge_gathered(const void* rec, int world, int64_t nq, int k, float* 
 // ---- the exact two-pass scan (kernel 10 + k_screen.hip) -----------------------------
 bool screen_supported(int D, int dtype);
 // int8 copy of tiles [tile0, tile0 + ntiles) (tiles_d == nullptr) or of the ntiles tiles listed in tiles_d
+// tmeta: per tile 16 B {f32 scale, u32 live word, 0, 0}
 void launch_screen_quantize(const void* X, int D, int dtype, int64_t tile0, int64_t ntiles, const int64_t* tiles_d,
-                            int8_t* codes, float* tscale, uint32_t* live, uint32_t* stats, hipStream_t st);
+                            int8_t* codes, void* tmeta, uint32_t* stats, hipStream_t st);
 MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k);
 size_t tau_bytes_screen(const MfmaPlan& p);
 void launch_screen_queries(const void* Q, int dtype, int D, int64_t nq, int64_t nq_pad, int8_t* Qc, float* qe2,
                            const uint32_t* stats, uint32_t* tau, uint32_t* gate, hipStream_t st);
-int launch_scan_screen(const MfmaPlan& p, const int8_t* codes, const float* tscale, const uint32_t* live, int nrows,
-                       int D, const int8_t* Qc, const float* qe2, int nq, uint32_t* tau, float* cs, int* cr,
-                       uint32_t* drops, hipStream_t st, const uint32_t* mask);
+int launch_scan_screen(const MfmaPlan& p, const int8_t* codes, const void* tmeta, const uint32_t* stats, int nrows, int D,
+                       const int8_t* Qc, const float* qe2, int nq, uint32_t* tau, float* cs, int* cr, uint32_t* drops,
+                       hipStream_t st, const uint32_t* mask);
 int launch_screen_select(const float* cs, const int* cr, const uint32_t* drops, int64_t n_lists, int list_len,
                          const float* qe2, const void* Q, const void* X, int D, int dtype, int64_t nq, int k,
                          int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec, uint32_t* gate, int* diag,

@@ -137,6 +137,7 @@ SIGNATURES = {
     "rfx_search_masked": ([_u64, _p, _i64, _i, _p, _i64, _p, _p, _p, _sz, _p], _i),
     "rfx_search_records": ([_u64, _p, _i64, _i, _p, _i64, _i64, _p, _p, _sz, _p], _i),
     "rfx_search_plan": ([_u64, _i64, _i, _pi], _i),
+    "rfx_search_timed": ([_u64, _p, _i64, _i, _p, _i64, _i64, _p, _p, _p, _p, _sz, _p, _p, _p], _i),
     "rfx_index_screen": ([_u64, _i, _p], _i),
     "rfx_index_screen_read": ([_u64, _i64, _i64, _p, _p, _p, _p], _i),
     "rfx_screen_diag": ([_u64, _i64, _i, _p, _p, _p], _i),

@@ -213,12 +213,13 @@ class DeviceIndex:
         return kern.value
 
     def screen_read(self, tile0: int, ntiles: int):
-        """(codes int8 [ntiles*32][dim], scales f32 [ntiles], live u32 [ntiles], stats f32 [2]) of the copy."""
+        """(codes int8 [ntiles*32][dim], scales f32 [ntiles], live u32 [ntiles], stats f32 [3]: max row norm,
+        max quantisation-error norm, max tile scale) of the copy."""
         import numpy as np
         codes = np.empty((ntiles * 32, self.dim), dtype=np.int8)
         scales = np.empty(ntiles, dtype=np.float32)
         live = np.empty(ntiles, dtype=np.uint32)
-        stats = np.empty(2, dtype=np.float32)
+        stats = np.empty(3, dtype=np.float32)
         with torch.cuda.device(self.device):
             check(lib.rfx_index_screen_read(self.handle, int(tile0), int(ntiles), codes.ctypes.data, scales.ctypes.data,
                                             live.ctypes.data, stats.ctypes.data))

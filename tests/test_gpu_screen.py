@@ -69,7 +69,7 @@ def test_int8_copy_bit_exact(rindex, dtype, d):
     assert codes.tobytes() == rc.tobytes()
     assert scales.tobytes() == rs.tobytes()
     assert live.tobytes() == rl.tobytes()
-    assert np.allclose(stats, rst, rtol=2e-7, atol=0)
+    assert np.allclose(stats[:2], rst[:2], rtol=2e-7, atol=0) and stats[2] == rst[2] == scales.max()
 
 
 @pytest.mark.parametrize("nq,k", [(256, 10), (100, 10), (300, 4), (256, 1)])

@@ -1,0 +1,15 @@
+#!/bin/bash
+# round 3: kernel-10 variants (launder, prefetch distance, ring) interleaved, then power/sclk per variant
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/r03f; mkdir -p $O
+timeout -k 10 400 python -u tools/k10_variants.py > $O/variants.json 2> $O/variants.err || { tail -5 $O/variants.err; exit 1; }
+cat $O/variants.json
+for v in 800 802 809 9; do
+  timeout -k 10 120 python -u tools/k10_variants.py --variants $v --seconds 8 > $O/run_$v.json 2> $O/run_$v.err &
+  pid=$!
+  sleep 14
+  for i in 1 2 3; do timeout -k 5 20 rocm-smi --showclocks --showpower >> $O/smi_$v.txt 2>&1; sleep 0.5; done
+  wait $pid || { echo "run $v failed"; tail -5 $O/run_$v.err; exit 1; }
+  echo "$v $(cat $O/run_$v.json) | $(grep -oE 'sclk clock level: [0-9]+: \([0-9]+Mhz\)|Power \(W\): [0-9.]+' $O/smi_$v.txt | tr '\n' ' ')"
+done
