@@ -22,7 +22,11 @@ Pinning:
     asserted values of the reference's tests (backend/tests/test_gemini_rag.py:40-93,
     backend/tests/test_chat_stream_helpers.py:37-75), extracted with `ast` by
     tests/golden/make_ref_boundary.py;
-  * the mock's response shape (mock_response, first_stream_text): restated from the source only;
+  * the mock's response shape (mock_response, first_stream_text, contents -> question): the
+    reference MockGeminiRag's own outputs for a fixed question list, tests/golden/ref_mock.json
+    (captured by importing it in the build container, tests/golden/make_ref_mock.py);
+  * the exact two-pass scan (screen.py): its int8 copy bit-exact on the GPU, its selection rule shown
+    on the CPU to return search.topk exactly (tests/test_screen_oracle.py);
   * the numeric path (synth/embed/search): no reference counterpart — parity unpinned against
     Gemini; pinned by its own committed fixtures (tests/golden/make_golden.py) and exact-arithmetic
     identities.

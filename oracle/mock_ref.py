@@ -9,9 +9,9 @@ local-GPU adapter's outputs have the reference structure.
 Pinning: extract_citations, citation_frame_payloads and finish_frame_payload are checked against
 the reference's own test vectors (tests/golden/ref_boundary.json, extracted from
 backend/tests/test_gemini_rag.py and backend/tests/test_chat_stream_helpers.py by
-tests/golden/make_ref_boundary.py).  mock_response / first_stream_text follow the reference source
-(SURVEY §8c lists the mock's outputs); no reference test calls MockGeminiRag, so those two are
-restated from the source only.
+tests/golden/make_ref_boundary.py).  mock_response / first_stream_text are pinned by the reference
+MockGeminiRag's own outputs for a fixed question list (tests/golden/ref_mock.json, captured by
+tests/golden/make_ref_mock.py; tests/test_ref_mock_golden.py).
 """
 import json
 from types import SimpleNamespace

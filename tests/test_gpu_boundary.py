@@ -73,3 +73,31 @@ def test_multi_store_union_on_gpu(golden_dir, tmp_path):
                 ref = float(orc._embed([h.text])[0] @ qv)
                 assert abs(h.score - ref) <= 1e-5, (h.text, h.score, ref)
             assert np.all(np.diff([h.score for h in hits]) <= 0)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_reference_mock_fixture_on_gpu(golden_dir, tmp_path, dtype):
+    """The reference mock's captured outputs (tests/golden/ref_mock.json, MockGeminiRag) against
+    LocalGpuRag on the HIP path at k = 1: the first stream chunk is identical; the second carries the
+    mock's attribute structure, citation keys, rank-0 index and the queried store."""
+    from rfx import store as rstore
+    from rfx.adapter import LocalGpuRag
+    from rfx.retriever import GpuRetriever
+    from test_ref_mock_golden import _contents, contained, ns_to_dict, shape
+
+    gold = json.load(open(os.path.join(golden_dir, "ref_mock.json")))
+    rstore.set_registry(rstore.StoreRegistry(root=str(tmp_path), device=0))
+    rag = LocalGpuRag(GpuRetriever(dtype=dtype), top_k=1)
+    st = rag.create_store("demo")
+    rag.upload_file(st, os.path.join(golden_dir, "sample_report.md"), display_name="sample-report.md")
+    for c in gold["cases"]:
+        if not c["store_names"]:
+            continue
+        chunks = list(rag.ask_stream(contents=_contents(c["question"]), store_names=[st], metadata_filter=None,
+                                     model="gemini-2.5-flash"))
+        assert ns_to_dict(chunks[0]) == c["stream"][0]
+        assert contained(shape(c["stream"][1]), shape(ns_to_dict(chunks[1])))
+        cits = rag.extract_citations_from_response(chunks[1])
+        assert [sorted(x) for x in cits] == [sorted(x) for x in c["citations"]]
+        assert cits[0]["index"] == 0 and cits[0]["store"] == st
+    rag.delete_store(st)
