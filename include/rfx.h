@@ -307,6 +307,17 @@ int rfx_ivf_search_rerank(rfx_ivf_t h, const void* queries_d, int64_t nq, int dt
                           int nprobe, int rerank_k, const void* rows_d, int rows_dtype,
                           float* out_scores_d, int64_t* out_rows_d, void* ws_d, size_t ws_bytes,
                           void* stream);
+/* The re-rank step alone, for a store row-sharded over several devices (rfx/sharded.py
+ * ShardedIvf; gemini_rag.py:463-469's file-search tool over an RFX_INDEX=ivf store): cand_d
+ * [nq][n_cand] holds GLOBAL row ids (< 0 = padding); the candidates in [row_lo, row_lo + n_rows)
+ * are re-scored in f32 against rows_d (this shard's rows: local row = global - row_lo), the others
+ * come back as (-inf, -1).  out_scores_d / out_rows_d [nq][n_cand] (global rows): the merge input.
+ * The same kernel and summation order as rfx_ivf_search_rerank, so a sharded store re-ranks its
+ * candidates bit-identically to one device. */
+int rfx_rerank_candidates(const void* queries_d, int64_t nq, int dtype, const void* rows_d,
+                          int rows_dtype, int64_t row_lo, int64_t n_rows, int dim,
+                          const int64_t* cand_d, int n_cand, float* out_scores_d,
+                          int64_t* out_rows_d, void* stream);
 /* int8 quantisation of rows (the IVF code format): codes [n][dim], inv [n] = amax / 127 */
 int rfx_quantize(const void* rows_d, int64_t n, int dim, int dtype, int8_t* codes_d, float* inv_d,
                  void* stream);

@@ -486,6 +486,26 @@ int rfx_ivf_search_rerank(rfx_ivf_t h, const void* queries_d, int64_t nq, int dt
   return RFX_OK;
 }
 
+// The re-rank step alone over one shard's rows (rfx/sharded.py ShardedIvf): candidates are global
+// rows, the shard owns [row_lo, row_lo + n_rows).  The same kernel as rfx_ivf_search_rerank.
+int rfx_rerank_candidates(const void* queries_d, int64_t nq, int dtype, const void* rows_d, int rows_dtype,
+                          int64_t row_lo, int64_t n_rows, int dim, const int64_t* cand_d, int n_cand,
+                          float* out_scores_d, int64_t* out_rows_d, void* stream) {
+  if (!valid_dtype(rows_dtype) || !valid_dtype(dtype)) return api_fail(RFX_EINVAL, "bad dtype");
+  if (nq < 0 || n_cand < 0 || dim <= 0 || row_lo < 0 || n_rows < 0)
+    return api_fail(RFX_EINVAL, "bad sizes (nq %lld, n_cand %d, dim %d, rows [%lld, +%lld))", (long long)nq, n_cand,
+                    dim, (long long)row_lo, (long long)n_rows);
+  if (nq == 0 || n_cand == 0) return RFX_OK;
+  if (!queries_d || !cand_d || !out_scores_d || !out_rows_d || (n_rows > 0 && !rows_d))
+    return api_fail(RFX_EINVAL, "null pointers");
+  hipStream_t st = (hipStream_t)stream;
+  if (rfx::ivf::launch_rerank(queries_d, dtype, rows_d, rows_dtype, dim, cand_d, nq, n_cand, out_scores_d, out_rows_d,
+                              st, row_lo, n_rows))
+    return api_fail(RFX_EUNSUPPORTED, "re-rank launch rejected");
+  IVF_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
 // Persistence: "RFXIVF01", {version 1, dim, nlist, trained}, rows, then the int8 centroids and
 // the per-row codes / scales / labels in insertion order.  Factors and posting lists are derived
 // (recomputed on load).  Written to path.tmp, then renamed.

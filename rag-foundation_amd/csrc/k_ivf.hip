@@ -635,34 +635,38 @@ namespace ivf {
 // ---- exact re-rank of IVF candidates against the original rows -----------------------------------
 // One block per query, one wave per candidate (strided): f32 dot of the query and the candidate's
 // original row (bf16 / f16 / f32, e.g. the brute-force store's buffer), wave reduction.  Rows < 0
-// (padding) stay -1 with score -inf, which the merge skips.
+// (padding) stay -1 with score -inf, which the merge skips.  Row-sharded use (rfx_rerank_candidates):
+// the candidates are global rows, X holds rows [row_lo, row_lo + n_rows); the others are padding here.
 template <int DTQ, int DTX>
 __global__ __launch_bounds__(256) void rerank_kernel(const void* __restrict__ Q, const void* __restrict__ X, int D,
-                                                     const int64_t* __restrict__ cand, int kc,
-                                                     float* __restrict__ out_s, int64_t* __restrict__ out_r) {
+                                                     const int64_t* __restrict__ cand, int kc, int64_t row_lo,
+                                                     int64_t n_rows, float* __restrict__ out_s,
+                                                     int64_t* __restrict__ out_r) {
   const int64_t q = blockIdx.x;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int c = w; c < kc; c += 4) {
     const int64_t r = cand[q * kc + c];
+    const int64_t lr = r - row_lo;
+    const bool own = r >= 0 && lr >= 0 && lr < n_rows;
     float acc = 0.f;
-    if (r >= 0)
-      for (int d = lane; d < D; d += 64) acc = fmaf(load_elem<DTQ>(Q, q * D + d), load_elem<DTX>(X, r * D + d), acc);
+    if (own)
+      for (int d = lane; d < D; d += 64) acc = fmaf(load_elem<DTQ>(Q, q * D + d), load_elem<DTX>(X, lr * D + d), acc);
 #pragma unroll
     for (int off = 32; off; off >>= 1) acc += __shfl_xor(acc, off);
     if (lane == 0) {
-      out_s[q * kc + c] = r >= 0 ? acc : -__builtin_inff();
-      out_r[q * kc + c] = r >= 0 ? r : -1;  // (negative rows are never live in the merge)
+      out_s[q * kc + c] = own ? acc : -__builtin_inff();
+      out_r[q * kc + c] = own ? r : -1;  // (negative rows are never live in the merge)
     }
   }
 }
 
 int launch_rerank(const void* Q, int dtq, const void* X, int dtx, int D, const int64_t* cand, int64_t nq, int kc,
-                  float* out_s, int64_t* out_r, hipStream_t st) {
+                  float* out_s, int64_t* out_r, hipStream_t st, int64_t row_lo, int64_t n_rows) {
   if (nq <= 0) return 0;
 #define RFX_RR(A, B)                                                                                        \
   if (dtq == A && dtx == B) {                                                                               \
-    hipLaunchKernelGGL((rerank_kernel<A, B>), dim3((unsigned)nq), dim3(256), 0, st, Q, X, D, cand, kc, out_s, \
-                       out_r);                                                                              \
+    hipLaunchKernelGGL((rerank_kernel<A, B>), dim3((unsigned)nq), dim3(256), 0, st, Q, X, D, cand, kc, row_lo, \
+                       n_rows, out_s, out_r);                                                               \
     return 0;                                                                                               \
   }
   RFX_RR(RFX_F32, RFX_F32) RFX_RR(RFX_F32, RFX_BF16) RFX_RR(RFX_F32, RFX_F16)

@@ -11,7 +11,9 @@
 //     'DVFS give-back' item 7); measured -2.4 % on kernel 5.  The epilogue's query-pair swap is one
 //     v_permlane16_swap per register pair.
 //   * Non-temporal corpus DMA (the corpus is read once per batch).
-//   * No ablation code in the production template (kernel 5's MODE bits live in the debug build).
+//   * The production instantiations are MODE 0 and kModeMask (row filter); the other MODE bits
+//     (below the template) are debug-build ablations (k6_dbg.hip, librfx_dbg.so) and compile
+//     out of the product library's instantiations.
 // Why not more: the launch runs at the board's power cap (rocm-smi: 1400 W package power, sclk
 // 1.8-1.95 GHz, profiles/r02_power_*), so its time is the batch's energy over the cap; measured
 // alternatives that traded cycles for energy (tools/k5_variants.py, steady-state 8-s bursts):
@@ -240,15 +242,15 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
     return f;
   };
 
-  // Schedule.  Stage h's pieces go out during stage h - 5, at k-steps 0 and 4, into the slot freed
-  // at stage h - 6's barrier.  Fragments are read one k-step ahead of their MFMAs; the stage-end
+  // Schedule.  Stage h's pieces go out during stage h - (RING - 1), at k-steps 0 and 4, into the
+  // slot freed at stage h - RING's barrier (production RING 4: during stage h - 3, slot of h - 4).  Fragments are read one k-step ahead of their MFMAs; the stage-end
   // wait + barrier sit at k-step KPS - 1, once every wave has issued (and, by lgkmcnt(0), received)
   // its last read of the stage.
   constexpr int PF = 1;
   constexpr int NF = PF + 1;
   constexpr int KB = KPS - PF;
   constexpr int AHEAD = RING - 1;
-  constexpr int YNG = (RING - 2) * kGPW;  // ops younger than the next stage (8 with 6 slots)
+  constexpr int YNG = (RING - 2) * kGPW;  // ops younger than the next stage (4 with the 4-slot ring)
   static_assert((NST * KPS) % NF == 0, "fragment rotation must realign every tile");
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // resident queries landed before the counted stream

@@ -125,7 +125,8 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
 // live), 2 = resident fragments NOT laundered (hipcc's own vmcnt waits stay in the loop), 4 = A
 // fragments prefetched 2 k-steps ahead (d 768 only), 8 = no corpus stream after the prologue (MFMA +
 // LDS only; wrong scores, timing only), 32 = count slow-path entries (threshold slot 15 of each
-// wave's first query).
+// wave's first query), 64 = the fast path on the store-wide integer bound (max tile scale) instead
+// of the tile's own scale, 128 = the epilogue in place at each tile's end (no alternating accumulators).
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
@@ -213,7 +214,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   };
 
   uint32_t thr = 0u, drop = 0u;
-  // Fast-path bounds on the raw i32 dot D (no per-tile data): every tile scale s_t <= smax, so a
+  // Debug MODE 64's fast path, bounds on the raw i32 dot D (no per-tile data): every tile scale s_t <= smax, so a
   // lane value with D < ibound(thr) has fl(D s_t) < thr - e2 and is never looked at (proof in
   // DESIGN §4.10).  ti_own: this lane's query (after the pair swap); ti_oth: the query the partner
   // lane (lane ^ 16) owns, whose values this lane also holds before the swap.
@@ -226,9 +227,20 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
     return qv >= 2.0e9f ? INT_MAX : (int)floorf(qv);
   };
   int ti_own = INT_MIN, ti_oth = INT_MIN;
+  // Production fast path: the slow path's own test, (float)D * s_t >= thr - e2, on the lane's max D
+  // per query with the tile's scale from the LDS metadata slot (one ds_read per tile).  Float
+  // multiplication by s_t >= 0 is monotone, so the max passes whenever any value would.  Against
+  // the store-wide smax bound it skips the tiles whose scale lies below smax (measured: 17 % of
+  // wave-tiles entered the slow path with the smax bound).
+  float tf_own = -__builtin_inff(), tf_oth = -__builtin_inff();
   auto set_bounds = [&]() {
-    ti_own = ibound(thr);
-    ti_oth = __shfl_xor(ti_own, 16);
+    if constexpr ((MODE & 64) != 0) {
+      ti_own = ibound(thr);
+      ti_oth = __shfl_xor(ti_own, 16);
+    } else {
+      tf_own = thr ? unord(thr) - e2 : -__builtin_inff();
+      tf_oth = __shfl_xor(tf_own, 16);
+    }
   };
   const bool odd = ((lane >> 4) & 1) != 0;
   const uint32_t slot_voff = (uint32_t)(q * kTauW + lst % KL) * 4u;
@@ -271,9 +283,55 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   Frag fr[NF];
 #pragma unroll
   for (int p = 0; p < PF; ++p) fr[p] = read_frag(0, p);
-  v4i32 acc4[4];  // [rb * 2 + qb]
-  for (int it = 0; it < nt; ++it) {
+  // Accumulators alternate between tiles: the epilogue of tile it - 1 runs right after tile it's
+  // first k-step of MFMAs (production), so its VALU / LDS work overlaps the matrix cores instead of
+  // waiting for the MFMA pipeline to drain at every tile end (debug MODE 128: epilogue in place).
+  v4i32 accA[4], accB[4];  // [rb * 2 + qb]
+  auto epilogue = [&](const int it, v4i32(&acc4)[4]) {
     const int tile = range + it * nblk;
+    // Fast path: the max D of each of the lane's two queries, scaled by the tile's scale, against the
+    // query's bound (qb 0 values in acc4[0], acc4[2]; qb 1 in acc4[1], acc4[3]).  Only when some lane of the wave
+    // may hold a row to look at: the tile's scale and live word (LDS metadata slot), the pair swap (even
+    // 16-lane row keeps query n, odd keeps 16 + n) and the exact fold.
+    int m0 = max3i(acc4[0][0], acc4[0][1], acc4[0][2]);
+    int m1 = max3i(acc4[1][0], acc4[1][1], acc4[1][2]);
+    m0 = max3i(m0, acc4[0][3], acc4[2][0]);
+    m1 = max3i(m1, acc4[1][3], acc4[3][0]);
+    m0 = max3i(m0, acc4[2][1], acc4[2][2]);
+    m1 = max3i(m1, acc4[3][1], acc4[3][2]);
+    m0 = max(m0, acc4[2][3]);
+    m1 = max(m1, acc4[3][3]);
+    bool hit;
+    if constexpr ((MODE & 64) != 0) {  // debug: the store-wide integer bound (no per-tile data)
+      hit = (odd ? m1 : m0) >= ti_own || (odd ? m0 : m1) >= ti_oth;
+    } else {
+      const float st_t = *(const float*)(lds + kMetaOff + (it % kMR) * 1024 + lane * 16);
+      hit = (float)(odd ? m1 : m0) * st_t >= tf_own || (float)(odd ? m0 : m1) * st_t >= tf_oth;
+    }
+    if constexpr ((MODE & 1) == 0) {
+      if (__builtin_amdgcn_ballot_w64(hit)) {
+        if constexpr ((MODE & 32) != 0)  // debug: count slow-path entries per wave (unused threshold slot 15)
+          if (lane == 0) atomicAdd(tau + (int64_t)(qg + w * kQW) * kTauW + 15, 1u);
+        const uint2 md = *(const uint2*)(lds + kMetaOff + (it % kMR) * 1024 + lane * 16);
+        const float st = __uint_as_float(md.x);
+        uint32_t lw = md.y;
+        if constexpr (MASK) lw &= mask[tile];
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const auto r = __builtin_amdgcn_permlane16_swap((uint32_t)acc4[2 * rb][i], (uint32_t)acc4[2 * rb + 1][i], false, false);
+            acc4[2 * rb][i] = (int)r[0];
+            acc4[2 * rb + 1][i] = (int)r[1];
+          }
+        fold_screen<KL>(acc4, st, lw >> (8 * half), Ls, thr, e2, drop, tile * kTM + 8 * half, tau_rsrc, slot_voff);
+        set_bounds();
+      }
+    } else if (hit && m0 == 12345 && m1 == 54321) {
+      Ls[0] = 1;
+    }
+  };
+  auto tile_body = [&](const int it, v4i32(&acc4)[4], v4i32(&accp)[4], const bool prev) {
     const int gbase = it * NST;
     if (it >= 2 && tau_refresh_tile(it - 2)) {
       thr = max(thr, tau_min<KL>(tq));
@@ -336,43 +394,28 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
           for (int qb = 0; qb < 2; ++qb)
             acc4[2 * rb + qb] = ks == 0 ? mfma_i8(cur.a[rb], bq[2 * ks + qb], v4i32{0, 0, 0, 0})
                                         : mfma_i8(cur.a[rb], bq[2 * ks + qb], acc4[2 * rb + qb]);
+        if constexpr ((MODE & 128) == 0)
+          if (s == 0 && kk == 0 && prev) epilogue(it - 1, accp);
       }
     }
 
-    // epilogue.  Fast path: the max D of each of the lane's two queries against its integer bound
-    // (qb 0 values in acc4[0], acc4[2]; qb 1 in acc4[1], acc4[3]).  Only when some lane of the wave
-    // may hold a row to look at: the tile's scale and live word (LDS metadata slot), the pair swap (even
-    // 16-lane row keeps query n, odd keeps 16 + n) and the exact fold.
-    int m0 = max3i(acc4[0][0], acc4[0][1], acc4[0][2]);
-    int m1 = max3i(acc4[1][0], acc4[1][1], acc4[1][2]);
-    m0 = max3i(m0, acc4[0][3], acc4[2][0]);
-    m1 = max3i(m1, acc4[1][3], acc4[3][0]);
-    m0 = max3i(m0, acc4[2][1], acc4[2][2]);
-    m1 = max3i(m1, acc4[3][1], acc4[3][2]);
-    m0 = max(m0, acc4[2][3]);
-    m1 = max(m1, acc4[3][3]);
-    const bool hit = (odd ? m1 : m0) >= ti_own || (odd ? m0 : m1) >= ti_oth;
-    if constexpr ((MODE & 1) == 0) {
-      if (__builtin_amdgcn_ballot_w64(hit)) {
-        if constexpr ((MODE & 32) != 0)  // debug: count slow-path entries per wave (unused threshold slot 15)
-          if (lane == 0) atomicAdd(tau + (int64_t)(qg + w * kQW) * kTauW + 15, 1u);
-        const uint2 md = *(const uint2*)(lds + kMetaOff + (it % kMR) * 1024 + lane * 16);
-        const float st = __uint_as_float(md.x);
-        uint32_t lw = md.y;
-        if constexpr (MASK) lw &= mask[tile];
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const auto r = __builtin_amdgcn_permlane16_swap((uint32_t)acc4[2 * rb][i], (uint32_t)acc4[2 * rb + 1][i], false, false);
-            acc4[2 * rb][i] = (int)r[0];
-            acc4[2 * rb + 1][i] = (int)r[1];
-          }
-        fold_screen<KL>(acc4, st, lw >> (8 * half), Ls, thr, e2, drop, tile * kTM + 8 * half, tau_rsrc, slot_voff);
-        set_bounds();
-      }
-    } else if (hit && m0 == 12345 && m1 == 54321) {
-      Ls[0] = 1;
+  };
+  if constexpr ((MODE & 128) != 0) {
+    for (int it = 0; it < nt; ++it) {
+      tile_body(it, accA, accB, false);
+      epilogue(it, accA);
+    }
+  } else {
+    int it = 0;
+    for (; it + 1 < nt; it += 2) {
+      tile_body(it, accA, accB, it > 0);
+      tile_body(it + 1, accB, accA, true);
+    }
+    if (it < nt) {
+      tile_body(it, accA, accB, it > 0);
+      epilogue(it, accA);
+    } else {
+      epilogue(it - 1, accB);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -163,7 +163,7 @@ int launch_list_scan(int K, int D, int m, int splits, const int8_t* codes, const
                      const int* pair_off, const int* pairs, int nprobe, const int8_t* qq, const float* qinv,
                      float* cs, int* cr, hipStream_t st);
 int launch_rerank(const void* Q, int dtq, const void* X, int dtx, int D, const int64_t* cand, int64_t nq, int kc,
-                  float* out_s, int64_t* out_r, hipStream_t st);
+                  float* out_s, int64_t* out_r, hipStream_t st, int64_t row_lo = 0, int64_t n_rows = INT64_MAX);
 }  // namespace ivf
 
 // error reporting shared by the C-ABI translation units (rfx_api.hip owns rfx_last_error)

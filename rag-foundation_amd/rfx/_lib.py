@@ -133,6 +133,7 @@ SIGNATURES = {
     "rfx_ivf_search_workspace_bytes": ([_u64, _i64, _i, _i, _psz], _i),
     "rfx_ivf_rerank_workspace_bytes": ([_u64, _i64, _i, _i, _i, _psz], _i),
     "rfx_ivf_search_rerank": ([_u64, _p, _i64, _i, _i, _i, _i, _p, _i, _p, _p, _p, _sz, _p], _i),
+    "rfx_rerank_candidates": ([_p, _i64, _i, _p, _i, _i64, _i64, _i, _p, _i, _p, _p, _p], _i),
     "rfx_ivf_search": ([_u64, _p, _i64, _i, _i, _i, _p, _p, _p, _sz, _p], _i),
     "rfx_search_masked": ([_u64, _p, _i64, _i, _p, _i64, _p, _p, _p, _sz, _p], _i),
     "rfx_search_records": ([_u64, _p, _i64, _i, _p, _i64, _i64, _p, _p, _sz, _p], _i),

@@ -213,6 +213,28 @@ class IvfIndex:
         self.set_centroids(torch.from_numpy(qc.copy()).to(self._dev()))
 
 
+def rerank_candidates(queries: torch.Tensor, rows_ptr: int, rows_dtype: str, row_lo: int, n_rows: int,
+                      cand: torch.Tensor, stream=None):
+    """Exact f32 re-score of global candidate rows cand [nq][n_cand] (int64, < 0 = padding) against
+    one shard's rows (device pointer to [n_rows][dim] of rows_dtype holding global rows
+    [row_lo, row_lo + n_rows)); candidates outside the shard come back (-inf, -1).
+    -> (scores f32 [nq][n_cand], rows int64 [nq][n_cand]) (rfx_rerank_candidates)."""
+    dt = {v: k for k, v in _lib.TORCH_DTYPES.items()}.get(queries.dtype)
+    if dt is None or queries.dim() != 2 or not queries.is_cuda:
+        raise ValueError("queries must be a cuda float32/bfloat16/float16 [nq][dim] tensor")
+    if cand.dtype != torch.int64 or cand.dim() != 2 or cand.shape[0] != queries.shape[0] or cand.device != queries.device:
+        raise ValueError("candidates must be int64 [nq][n_cand] on the queries' device")
+    q, c = queries.contiguous(), cand.contiguous()
+    nq, nc = c.shape
+    out_s = torch.empty((nq, nc), dtype=torch.float32, device=q.device)
+    out_r = torch.empty((nq, nc), dtype=torch.int64, device=q.device)
+    with torch.cuda.device(q.device):
+        check(lib.rfx_rerank_candidates(ptr(q), nq, _lib.DTYPE_CODES[dt], ctypes.c_void_p(int(rows_ptr)),
+                                        _lib.DTYPE_CODES[rows_dtype], int(row_lo), int(n_rows), q.shape[1], ptr(c),
+                                        nc, ptr(out_s), ptr(out_r), stream_ptr(stream)))
+    return out_s, out_r
+
+
 def quantize(rows: torch.Tensor, stream=None):
     """int8 codes [n][dim] + inv scales [n] of rows (the IVF code format)."""
     dt = {v: k for k, v in _lib.TORCH_DTYPES.items()}[rows.dtype]

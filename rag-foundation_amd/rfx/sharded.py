@@ -6,7 +6,11 @@ unchanged (RFX_DEVICES=0,1,...,7; gemini_rag.py:463-469 store -> shards, :721-72
 Layout: shard i holds the contiguous global rows [base_i, base_i + rows_i); the bases are fixed
 when the store is first loaded (split evenly, at multiples of 32 rows so a row-mask word never
 straddles two shards) and rows appended later go to the last shard; when the last shard grows past
-twice the mean of the others the split is redone from the store's row file.
+twice the mean of the others the split is redone device to device (_resplit: shard 0 keeps its
+rows and appends, every other shard is rebuilt from peer-to-peer copies of the old shards' rows;
+nothing is re-read from disk).
+IVF stores (RFX_INDEX=ivf, config 5) keep one IVF list set per shard under the store's one coarse
+quantiser (ShardedIvf below); a search is bit-identical to the same store on one device.
 A search: the batch's queries go to every shard's device, each shard runs the fused scan + its
 merge into [nq][k] records with its base added (rfx_topk_merge_records), one RCCL all-gather over
 the process's devices (rfx_allgather_records on an ncclCommInitAll group), one rfx_merge_gathered.
@@ -34,7 +38,7 @@ def parse_devices(spec: str):
 
 
 class ShardedIndex:
-    supports_ivf = False  # IVF stores keep the exact scan when row-sharded (rfx.store)
+    supports_ivf = True  # IVF stores: ShardedIvf (new_ivf), one list set per shard
 
     def __init__(self, dim, dtype, devices):
         if not devices:
@@ -45,6 +49,7 @@ class ShardedIndex:
         self.shards = [DeviceIndex(self.dim, dtype, d) for d in self.devices]
         self.bases = [0] * len(self.shards)
         self._split = False
+        self.generation = 0  # bumped whenever the shard layout changes (ShardedIvf rebuilds its lists)
         self._tombs = []  # tombstoned global rows (re-applied after a re-split)
         distinct = len(set(self.devices)) == len(self.devices)
         self.comm = RcclComm.for_devices(self.devices) if distinct and len(self.devices) > 1 else None
@@ -68,15 +73,19 @@ class ShardedIndex:
         return sid, rows - np.asarray(self.bases)[sid]
 
     # ---- loads / writes --------------------------------------------------------------------------
-    def _do_split(self, upto):
+    def _cuts(self, upto):
         n = len(self.shards)
         # every base a multiple of ALIGN, also when upto itself is not (a reader opening a store after
         # a small first upload): mask_tensor slices whole mask words per shard
         top = (upto // ALIGN) * ALIGN
-        cuts = [min(top, -(-(i * upto // n) // ALIGN) * ALIGN) for i in range(n)] + [upto]
-        for i in range(n):
+        return [min(top, -(-(i * upto // n) // ALIGN) * ALIGN) for i in range(n)] + [upto]
+
+    def _do_split(self, upto):
+        cuts = self._cuts(upto)
+        for i in range(len(self.shards)):
             self.bases[i] = cuts[i]
         self._split = True
+        self.generation += 1
         return cuts
 
     def rows_sync(self, path: str, upto: int) -> None:
@@ -98,12 +107,39 @@ class ShardedIndex:
             self._resplit(path, upto)
 
     def _resplit(self, path, upto):
-        for sh in self.shards:
+        """Rebalance device to device (ADVICE/VERDICT r2: no reload from disk).  The new cuts only
+        move forward (the store grew), so shard 0 keeps its rows and appends its new tail; shard
+        i > 0 is rebuilt from peer copies of the old shards' rows [cut_i, cut_i+1) in 1M-row pieces.
+        The new shards are complete before the old ones are closed (callers hold self._lock)."""
+        old, old_bases = self.shards, list(self.bases)
+        cuts = self._cuts(upto)
+        span = 1 << 20
+
+        def copy_into(dst, lo, hi):
+            for j, (sh, b) in enumerate(zip(old, old_bases)):
+                a, e = max(lo, b), min(hi, b + sh.rows)
+                for r0 in range(a, e, span):
+                    n = min(span, e - r0)
+                    dst.add(sh.read(r0 - b, n).to(torch.device("cuda", dst.device)))
+
+        new = [old[0]]
+        try:
+            copy_into(old[0], old_bases[0] + old[0].rows, cuts[1])
+            for i in range(1, len(old)):
+                sh = DeviceIndex(self.dim, self.dtype, self.devices[i], capacity=max(cuts[i + 1] - cuts[i], 1))
+                new.append(sh)
+                copy_into(sh, cuts[i], cuts[i + 1])
+        except BaseException:
+            for sh in new[1:]:
+                sh.close()
+            raise
+        for sh in old[1:]:
             sh.close()
-        self.shards = [DeviceIndex(self.dim, self.dtype, d) for d in self.devices]
-        self._split = False
-        self._rows_sync(path, upto)
-        if self._tombs:
+        self.shards = new
+        for i in range(len(new)):
+            self.bases[i] = cuts[i]
+        self.generation += 1
+        if self._tombs:  # a copied tombstoned row is a NaN row: mark it dead in its new shard too
             self._tombstone(np.concatenate(self._tombs))
 
     def add(self, vecs: torch.Tensor) -> int:
@@ -182,6 +218,15 @@ class ShardedIndex:
                                              sorted=True)
             recs.append(rec)
         st0 = self._streams[0]
+        s, r = merge_gathered(self._exchange(recs, nq, k)[0], k, stream=st0)
+        src.wait_stream(st0)
+        return s, r
+
+    def _exchange(self, recs, nq, k, everywhere=False):
+        """Per-shard [nq][k][2] records -> the gathered [G][nq][k][2] records: on device 0 (list of
+        one), or with everywhere=True on every shard's device (list per shard, ordered on that
+        shard's stream).  Distinct devices: one RCCL all-gather; logical shards: a stack on stream 0."""
+        st0 = self._streams[0]
         if self.comm is not None:
             outs = []
             for d, st in zip(self.devices, self._streams):
@@ -189,14 +234,134 @@ class ShardedIndex:
                 o.record_stream(st)
                 outs.append(o)
             self.comm.allgather_records(recs, outs, self._streams)
-            gathered = outs[0]
-        else:
-            for st in self._streams[1:]:
-                st0.wait_stream(st)
-            with torch.cuda.stream(st0):
-                gathered = torch.stack(recs)
-            for rec in recs:
-                rec.record_stream(st0)
-        s, r = merge_gathered(gathered, k, stream=st0)
-        src.wait_stream(st0)
-        return s, r
+            return outs if everywhere else outs[:1]
+        for st in self._streams[1:]:
+            st0.wait_stream(st)
+        with torch.cuda.stream(st0):
+            gathered = torch.stack(recs)
+        for rec in recs:
+            rec.record_stream(st0)
+        if not everywhere:
+            return [gathered]
+        for st in self._streams[1:]:  # logical shards share device 0: the same tensor, after stream 0
+            st.wait_stream(st0)
+            gathered.record_stream(st)
+        return [gathered] * len(self.shards)
+
+    # ---- IVF (config 5) --------------------------------------------------------------------------
+    def new_ivf(self, nlist):
+        """The IVF index of an RFX_INDEX=ivf store over these shards (rfx.store._new_ivf)."""
+        return ShardedIvf(self, nlist)
+
+
+class ShardedIvf:
+    """IVF-Flat int8 over a ShardedIndex (SURVEY §8 config 5 behind the drop-in adapter;
+    gemini_rag.py:463-469): one coarse quantiser (the store's committed centroids, loaded on every
+    shard's device), each shard holding its rows' part of every posting list.  The interface is
+    rfx.ivf.IvfIndex's as rfx.store uses it (train_from, centroid_bytes, load_centroids, add_from,
+    rows, search_index, close).
+
+    A search is bit-identical to rfx_ivf_search_rerank on one device holding all rows:
+      1. every shard: its rerank_k best rows by int8 score (rfx_ivf_search; score desc, row asc),
+         as records with the shard's base added;
+      2. exchange + merge of those records = the store's global rerank_k best (the union of the
+         per-shard lists contains them, and the ranking rule is the same), on every shard's device;
+      3. every shard re-scores the global candidates it owns against its rows (rfx_rerank_candidates:
+         the one-device re-rank kernel), keeps its top k as records;
+      4. exchange + merge = the top k of the re-scored global candidates.
+    Two exchanges of nq * k_ * 16 B per shard (k_ = rerank_k, then k)."""
+
+    def __init__(self, sidx, nlist):
+        self.sidx, self.nlist, self.dim = sidx, int(nlist), sidx.dim
+        self.device = sidx.device
+        self.parts, self._gen, self._raw = [], None, None
+
+    def _fresh_parts(self):
+        from .ivf import IvfIndex
+        for p in self.parts:
+            p.close()
+        self.parts = [IvfIndex(self.dim, self.nlist, d) for d in self.sidx.devices]
+        if self._raw is not None:
+            for p in self.parts:
+                p.load_centroids(self._raw)
+        self._gen = self.sidx.generation
+
+    @property
+    def rows(self) -> int:
+        """Rows in the lists; -1 while the shard layout changed since they were built (not ready)."""
+        if self._gen != self.sidx.generation or len(self.parts) != len(self.sidx.shards):
+            return -1
+        return sum(p.rows for p in self.parts)
+
+    def train_from(self, index, row_ids, iters: int = 10) -> None:
+        from .ivf import IvfIndex
+        t = IvfIndex(self.dim, self.nlist, self.device)
+        try:
+            t.train_from(index, row_ids, iters)  # index.read: global rows, gathered onto device 0
+            self._raw = t.centroid_bytes()
+        finally:
+            t.close()
+        self._fresh_parts()
+
+    def centroid_bytes(self) -> bytes:
+        if self._raw is None:
+            raise ValueError("untrained")
+        return self._raw
+
+    def load_centroids(self, raw: bytes) -> None:
+        self._raw = bytes(raw)
+        self._fresh_parts()
+
+    def add_from(self, index, upto: int) -> None:
+        """Assign every shard's rows not yet in its lists (upto: the store's rows, all on shards)."""
+        with self.sidx._lock:
+            if self._gen != self.sidx.generation or len(self.parts) != len(self.sidx.shards):
+                self._fresh_parts()  # the layout changed: rebuild the lists from the shards' rows
+            for p, sh in zip(self.parts, self.sidx.shards):
+                p.add_from(sh, sh.rows)
+
+    def search_index(self, queries: torch.Tensor, k: int, nprobe: int, index=None, rerank_k: int = None, stream=None):
+        from .ivf import rerank_candidates
+        sidx = self.sidx
+        rk = max(int(k), 16) if rerank_k is None else int(rerank_k)
+        with sidx._lock:
+            if self.rows != sidx.rows:
+                raise RuntimeError("IVF lists are behind the shards (add_from first)")
+            nq = queries.shape[0]
+            src = torch.cuda.current_stream(queries.device)
+            qs, recs = [], []
+            for p, sh, base, d, st in zip(self.parts, sidx.shards, sidx.bases, sidx.devices, sidx._streams):
+                st.wait_stream(src)
+                with torch.cuda.device(d), torch.cuda.stream(st):
+                    q = queries.to(torch.device("cuda", d), non_blocking=True)
+                    s, r = p.search(q, rk, nprobe, stream=st)
+                    recs.append(topk_merge_records(s, r, rk, row_offset=base, stream=st))
+                qs.append(q)
+            cands = self._merge_each(sidx._exchange(recs, nq, rk, everywhere=True), rk)
+            recs2 = []
+            for q, sh, base, d, st, c in zip(qs, sidx.shards, sidx.bases, sidx.devices, sidx._streams, cands):
+                with torch.cuda.device(d), torch.cuda.stream(st):
+                    rs, rr = rerank_candidates(q, sh.data_ptr(), sh.dtype, base, sh.rows, c, stream=st)
+                    recs2.append(topk_merge_records(rs, rr, k, stream=st))
+            st0 = sidx._streams[0]
+            s, r = merge_gathered(sidx._exchange(recs2, nq, k)[0], k, stream=st0)
+            src.wait_stream(st0)
+            return s, r
+
+    def _merge_each(self, gathered, k):
+        """The global candidate rows on every shard's device (one merge per distinct tensor)."""
+        out, memo = [], {}
+        for g, st in zip(gathered, self.sidx._streams):
+            if id(g) not in memo:
+                memo[id(g)] = (merge_gathered(g, k, stream=st)[1], st)
+            rows, mst = memo[id(g)]
+            if mst is not st:  # logical shards: the one merge, ordered before this shard's stream
+                st.wait_stream(mst)
+                rows.record_stream(st)
+            out.append(rows)
+        return out
+
+    def close(self) -> None:
+        for p in self.parts:
+            p.close()
+        self.parts = []

@@ -334,10 +334,13 @@ class LocalStore:
         return self.spec.get("kind") == "ivf" and getattr(self.index, "supports_ivf", True)
 
     def _new_ivf(self):
-        if self.ivf_factory is None:
-            from .ivf import IvfIndex
-            LocalStore.ivf_factory = IvfIndex
-        return self.ivf_factory(self.dim, int(self.spec["nlist"]), self.device)
+        nlist = int(self.spec["nlist"])
+        if self.ivf_factory is not None:  # injected (host tests)
+            return self.ivf_factory(self.dim, nlist, self.device)
+        if hasattr(self.index, "new_ivf"):  # row-sharded store: one list set per shard (rfx.sharded)
+            return self.index.new_ivf(nlist)
+        from .ivf import IvfIndex
+        return IvfIndex(self.dim, nlist, self.device)
 
     def _drop_ivf(self):
         if self.ivf is not None:

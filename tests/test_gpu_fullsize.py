@@ -60,7 +60,22 @@ def test_cfg3_fullsize_headline_kernel(rindex):
     assert ix.plan(nq, k)[0] == 6, "cfg3 must run the headline kernel"
     s, r = ix.search(q, k)
     torch.cuda.synchronize()
-    oracle_check(ix, n, q, s, r, k)
+    ref_s, ref_r = oracle_check(ix, n, q, s, r, k)
+    # the exact two-pass scan bench.py times by default (int8 screen kernel 10 + exact re-score):
+    # the same oracle result for all 256 queries, with the fallback NOT taken (the screen answered)
+    ix.enable_screen(1)
+    assert ix.search_plan(nq, k) == 10
+    ws = torch.empty(ix.workspace_bytes(nq, k), dtype=torch.uint8, device=q.device)
+    s3, r3 = ix.search(q, k, workspace=ws)
+    torch.cuda.synchronize()
+    diag, fell_back = ix.screen_diag(nq, k, ws)
+    assert not fell_back and (diag[:, 1] >= k).all(), (fell_back, diag[:, 1].min())
+    q64 = host_f32(q).astype(np.float64)
+    probs = osearch.check_topk(s3.cpu().numpy(), r3.cpu().numpy(), ref_s, ref_r,
+                               lambda qi, rows: np.array([host_f32(ix.read(int(x), 1))[0].astype(np.float64) @ q64[qi]
+                                                          for x in rows]), tol=TOL, tie_band=TIE)
+    assert not probs, probs[:5]
+    ix.enable_screen(0)
     # an independent kernel over the same rows: the VALU scan, 8 queries per launch
     parts = [ix.search(q[i:i + 8], k) for i in range(0, nq, 8)]
     assert ix.plan(8, k)[0] == 0
@@ -82,5 +97,14 @@ def test_cfg4_shard_fullsize(rindex):
     assert kern == 8, kern
     s, r = ix.search(q, k)
     torch.cuda.synchronize()
-    oracle_check(ix, n, q, s, r, k)
+    ref_s, ref_r = oracle_check(ix, n, q, s, r, k)
+    # the two-pass scan at d 1024 (kernel 10's 1024 instantiation): the same oracle result
+    ix.enable_screen(1)
+    assert ix.search_plan(nq, k) == 10
+    s3, r3 = ix.search(q, k)
+    q64 = host_f32(q).astype(np.float64)
+    probs = osearch.check_topk(s3.cpu().numpy(), r3.cpu().numpy(), ref_s, ref_r,
+                               lambda qi, rows: np.array([host_f32(ix.read(int(x), 1))[0].astype(np.float64) @ q64[qi]
+                                                          for x in rows]), tol=TOL, tie_band=TIE)
+    assert not probs, probs[:5]
     ix.close()

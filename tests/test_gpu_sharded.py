@@ -125,3 +125,76 @@ def test_rccl_group_communicator_one_device():
     torch.cuda.synchronize()
     assert torch.equal(out[0], rec)
     comm.close()
+
+
+def test_sharded_resplit_device_to_device(tmp_path):
+    """Growth past twice the mean re-splits device to device (no row-file reload): shard 0 keeps its
+    rows, the others are rebuilt from peer copies; the result equals one index, tombstones kept."""
+    from rfx.index import DeviceIndex
+    from rfx.sharded import ShardedIndex
+
+    whole = DeviceIndex(768, "bf16", 0)
+    whole.add_synthetic(4, 9000)
+    path = str(tmp_path / "rows.rfx")
+    whole.rows_append(path, 0)
+    sh = ShardedIndex(768, "bf16", [0, 0, 0])
+    sh.rows_sync(path, 9000)
+    gen0, first = sh.generation, sh.shards[0]
+    sh.tombstone([17, 4000, 8999])
+    whole.tombstone([17, 4000, 8999])
+    whole.add_synthetic(4, 21000, gen_row0=9000)
+    whole.rows_append(path, 9000)
+    sh.rows_sync(path, 30000)  # last shard 3000 + 21000 rows > 2x the others' mean: re-split
+    assert sh.generation > gen0 and sh.shards[0] is first
+    assert all(b % 32 == 0 for b in sh.bases) and sh.rows == 30000
+    assert max(s.rows for s in sh.shards) - min(s.rows for s in sh.shards) <= 64
+    assert sh.live_rows == whole.live_rows
+    q = whole.read(100, 200)[::2].contiguous()
+    for nq in (100, 3):
+        a = whole.search(q[:nq], 10)
+        b = sh.search(q[:nq], 10)
+        assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0])
+    assert torch.equal(sh.read(0, 30000).view(torch.int16), whole.read(0, 30000).view(torch.int16))
+
+
+def test_sharded_ivf_store_equals_unsharded(tmp_path):
+    """An RFX_INDEX=ivf store read through 4 logical shards (rfx.sharded.ShardedIvf: one list set
+    per shard under the committed centroids, two record exchanges) answers bit-identically to the
+    same store on one device, before and after growth that re-splits the shards."""
+    from rfx import ivf as rivf
+    from rfx import store as rstore
+    from rfx.sharded import ShardedIndex, ShardedIvf
+
+    dim, spec = 768, {"kind": "ivf", "nlist": 32, "nprobe": 8, "train_min": 4000}
+    root = str(tmp_path)
+    st = rstore.StoreRegistry(root=root, device=0).create("ivf-sh", dim, "bf16", spec=spec)
+    docs = [rivf.synth_clustered(7, 48, 200 + i, 1500 * i, 1500, dim, "bf16") for i in range(3)]
+    fids = [st.add_document([f"d{i}-{j}" for j in range(1500)], v, f"d{i}.md")[0] for i, v in enumerate(docs)]
+    st.delete_file(fids[1])
+    st.add_document([f"e-{j}" for j in range(3000)], rivf.synth_clustered(7, 48, 300, 0, 3000, dim, "bf16"), "e.md")
+    assert st.ivf_ready()
+    preg = rstore.StoreRegistry(root=root, device=0)
+    sreg = rstore.StoreRegistry(root=root, device=0, devices="0x4")
+    plain, shard = preg.get(st.name), sreg.get(st.name)
+    assert isinstance(shard.index, ShardedIndex) and isinstance(shard.ivf, ShardedIvf)
+    assert plain.ivf_ready() and shard.ivf_ready() and shard.ivf_id == plain.ivf_id
+    q = rivf.synth_clustered(7, 48, 999, 0, 70, dim, "bf16")
+
+    def same(k):
+        a_s, a_r = plain.search(q, k)
+        b_s, b_r = shard.search(q, k)
+        assert np.array_equal(a_r.numpy(), b_r.numpy())
+        assert np.array_equal(a_s.numpy().view(np.uint32), b_s.numpy().view(np.uint32))
+        assert not np.isin(a_r.numpy(), np.arange(1500, 3000)).any()  # the deleted document
+
+    for k in (1, 10, 20):
+        same(k)
+    # growth: the sharded reader's last shard passes twice the mean -> device-to-device re-split,
+    # the lists are rebuilt on the new layout (26,000 live rows < 8x the trained 4,500: no retrain)
+    gen = shard.index.generation
+    st.add_document([f"g-{j}" for j in range(20000)], rivf.synth_clustered(7, 48, 400, 0, 20000, dim, "bf16"), "g.md")
+    plain, shard = preg.get(st.name), sreg.get(st.name)
+    assert shard.index.generation > gen and shard.ivf_id == plain.ivf_id
+    assert shard.ivf_ready() and plain.ivf_ready()
+    for k in (5, 10):
+        same(k)

@@ -3,7 +3,8 @@ corpus in bursts of back-to-back launches, variants interleaved over rounds (the
 settles per workload; cdna_hip_programming.md §5.4 rule 24).
 
 variant = 100 * RING + MODE (k10_dbg.hip): RING in {4, 6, 8, 10, 12}; MODE 1 = no top-k fold,
-8 = no corpus stream after the prologue, 9 = both; 9 alone = a plain streaming read of the int8 copy."""
+8 = no corpus stream after the prologue, 9 = both; 32 = count slow-path entries (reported, not
+timed); 64 = the store-wide integer fast-path bound."""
 import argparse
 import ctypes
 import json
@@ -62,18 +63,18 @@ if a.seconds > 0:  # steady state of ONE variant (rocm-smi samples power / sclk 
     torch.cuda.synchronize()
     print(json.dumps({"variant": v, "launches": n, "ms_per_launch": round(e0.elapsed_time(e1) / n, 4)}))
     sys.exit(0)
-if 832 in variants:  # slow-path entries of one launch (MODE 32 counter)
-    cnt = _lib.lib.rfx_dbg_screen_counts
-    cnt.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
-    cnt.restype = ctypes.c_int
-    launch(832)
+cnt = _lib.lib.rfx_dbg_screen_counts
+cnt.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
+cnt.restype = ctypes.c_int
+for v in [v for v in variants if (v % 100) & 32]:  # slow-path entries of one launch (MODE 32 counter)
+    launch(v)
     torch.cuda.synchronize()
     n = ctypes.c_uint64()
     _lib.check(cnt(ix.handle, a.nq, a.k, _lib.ptr(ws), ctypes.byref(n)))
     ntiles = -(-a.rows // 32)
-    print(json.dumps({"slow_path_wave_entries": n.value, "wave_tiles": ntiles * 8,
+    print(json.dumps({"variant": v, "slow_path_wave_entries": n.value, "wave_tiles": ntiles * 8,
                       "frac": round(n.value / (ntiles * 8), 5)}))
-    variants.remove(832)
+variants = [v for v in variants if not (v % 100) & 32]
 res = {v: [] for v in variants}
 for rnd in range(a.rounds):
     for v in (variants if rnd % 2 == 0 else variants[::-1]):
