@@ -271,12 +271,17 @@ def main():
 
     # algorithmic bytes of one scan launch on the largest shard: rows read once,
     # queries read once, (score,row) results written once.  The two-pass scan's kernel 10 reads the
-    # int8 codes (dim B per row), one scale + one live word per 32-row tile and the int8 query codes:
-    # its roofline is priced on THOSE bytes, not on the bf16 rows it does not read.
+    # int8 codes (dim B per row), the 16-B record {scale, live word} of every 32-row tile, the int8
+    # query codes and their bounds, and writes its candidate lists (KL (score, row) pairs per query
+    # and list) and one drop word per (query, list): its roofline is priced on THOSE bytes, not on
+    # the bf16 rows it does not read.
     n_max = rdist.shard_range(a.rows, 0, world)[1]
     nq_pad = -(-a.nq // 256) * 256
     if kern == 10:
-        alg_bytes = n_max * a.dim + (-(-n_max // 32)) * 8 + nq_pad * a.dim + nq_pad * 4 + a.nq * a.k * 12
+        n_lists = 2 * min(256 // max(1, nq_pad // 256), -(-n_max // 32))
+        kl = 4 if a.k <= 4 else 10
+        alg_bytes = (n_max * a.dim + (-(-n_max // 32)) * 16 + nq_pad * a.dim + nq_pad * 4
+                     + a.nq * n_lists * (kl * 8 + 4))
     else:
         alg_bytes = n_max * a.dim * esz + a.nq * a.dim * esz + a.nq * a.k * 12
     achieved = alg_bytes / (scan_ms * 1e-3) / 1e9
@@ -335,8 +340,7 @@ def main():
         # the bf16 queries, the survivors' bf16 rows) — what one batch costs in HBM traffic
         diag, fb = ixs[(a.steps - 1) % copies].screen_diag(a.nq, a.k, ws)
         sv = diag[:, 1]
-        n_lists = 2 * min(256 // max(1, nq_pad // 256), -(-n_max // 32))
-        sel_bytes = int(a.nq * n_lists * (10 * 8 + 4) + a.nq * a.dim * esz + max(int(sv.sum()), 0) * a.dim * esz)
+        sel_bytes = int(a.nq * n_lists * (kl * 8 + 4) + a.nq * a.dim * esz + max(int(sv.sum()), 0) * a.dim * esz)
         step_bytes = alg_bytes + sel_bytes
         result["two_pass"] = {
             "int8_copy_build_s": round(build_s / copies, 3), "int8_copy_bytes": n_max * a.dim,

@@ -12,6 +12,7 @@ from . import filters
 from .batcher import GroupBatcher
 from .embedder import DEFAULT_MAX_TOKENS, DEFAULT_OVERLAP, Embedder
 from .store import registry as default_registry
+from . import union as runion
 
 
 @dataclass
@@ -40,13 +41,16 @@ def _chunking(cfg):
 # (device, dim) and per store — or no two requests would ever share a batch.
 _STATE_LOCK = threading.Lock()
 _EMBEDDERS = {}
-_BATCHERS = {}  # (store name, filter key, registry id) -> GroupBatcher
+_BATCHERS = {}  # (store name | tuple of names, filter key, registry id) -> GroupBatcher
+_UNIONS = {}    # (tuple of names, registry id) -> UnionView (rfx.union), rebuilt when a member changes
 
 
 def _purge_batchers(name):
     with _STATE_LOCK:
-        for key in [k for k in _BATCHERS if k[0] == name]:
+        for key in [k for k in _BATCHERS if k[0] == name or (isinstance(k[0], tuple) and name in k[0])]:
             del _BATCHERS[key]
+        for key in [k for k in _UNIONS if name in k[0]]:
+            _UNIONS.pop(key).close()
 
 
 class GpuRetriever:
@@ -62,6 +66,9 @@ class GpuRetriever:
         self.dtype = os.environ.get("RFX_DTYPE", "bf16") if dtype is None else dtype
         # micro-batching of concurrent questions per store (RFX_BATCH=0 disables)
         self.batching = os.environ.get("RFX_BATCH", "1") != "0"
+        # a question over several stores: one scan of their union (rfx.union; RFX_UNION=0 disables)
+        self.union = os.environ.get("RFX_UNION", "1") != "0"
+        self.last_path = None  # "union" | "per-store" (tests, diagnostics)
 
     @property
     def registry(self):
@@ -147,15 +154,94 @@ class GpuRetriever:
             return self._batcher(name, metadata_filter).submit((question, int(k)))
         return self._run_batch(name, metadata_filter, [(question, int(k))])[0]
 
+    # ---- several stores in one launch (rfx.union) ------------------------------------------------
+    def _union_view(self, names, stores):
+        key = (tuple(names), id(self.registry))
+        want = runion.union_key(stores)
+        with _STATE_LOCK:
+            v = _UNIONS.get(key)
+            if v is not None and v.key == want:
+                return v
+            if v is not None:
+                _UNIONS.pop(key).close()
+            if len(_UNIONS) >= 64:
+                for old in _UNIONS.values():
+                    old.close()
+                _UNIONS.clear()
+            if self.registry.on_evict.count(_purge_batchers) == 0:
+                self.registry.on_evict.append(_purge_batchers)
+            v = runion.UnionView(stores)
+            _UNIONS[key] = v
+            return v
+
+    def _run_union_batch(self, names, metadata_filter, items):
+        """Batch runner over a store list: one embedding GEMM, one scan + merge of the members'
+        union.  Returns per item [(score, member index, row, store)] or None per item when the
+        list is not eligible (then the caller takes the per-store path)."""
+        stores = [self.registry.get(n) for n in names]
+        if any(st is None for st in stores) or not runion.eligible(stores):
+            return [None] * len(items)
+        locked = sorted(set(stores), key=lambda st: st.name)  # one global order: no lock-order deadlock
+        for st in locked:  # members hold their locks while the view is built and searched
+            st.lock.acquire()
+        try:
+            view = self._union_view(names, stores)
+            mask = view.row_mask(stores, metadata_filter) if metadata_filter is not None else None
+            if metadata_filter is not None and mask is None:
+                return [[] for _ in items]
+            kmax = max(k for _, k in items)
+            with torch.cuda.device(view.device):
+                q = self.embedder(view.dim).embed_texts([t for t, _ in items], view.dtype)
+                s, r = view.index.search(q, kmax, row_mask=mask)
+                s, r = s.cpu().numpy(), r.cpu().numpy()
+            si, lr = view.locate(r)
+            out = []
+            for i, (_, k) in enumerate(items):
+                out.append([(float(s[i, j]), int(si[i, j]), int(lr[i, j]), stores[si[i, j]])
+                            for j in range(k) if r[i, j] >= 0])
+            return out
+        finally:
+            for st in reversed(locked):
+                st.lock.release()
+
+    def _search_union(self, names, question, k, filt):
+        if self.batching:
+            key = (tuple(names), filters.filter_key(filt), id(self.registry))
+            with _STATE_LOCK:
+                b = _BATCHERS.get(key)
+                if b is None:
+                    b = GroupBatcher(lambda items, n=tuple(names), f=filt: self._run_union_batch(n, f, items),
+                                     max_batch=256)
+                    if len(_BATCHERS) >= 4096:
+                        _BATCHERS.clear()
+                    _BATCHERS[key] = b
+            return b.submit((question, int(k)))
+        return self._run_union_batch(tuple(names), filt, [(question, int(k))])[0]
+
     def search(self, store_names, question, k, metadata_filter=None):
         """Top-k hits over the union of the named stores, rank order (score desc, store order,
-        row asc).  metadata_filter: {key: scalar | [scalars]} over upload metadata (rfx.filters)."""
+        row asc).  metadata_filter: {key: scalar | [scalars]} over upload metadata (rfx.filters).
+        Several flat stores on one device: one scan of their union (rfx.union)."""
         k = int(k)
         if not 1 <= k <= 64:
             raise ValueError(f"top_k={k} out of range [1, 64]")
         filt = filters.check_filter(metadata_filter)
+        names = list(dict.fromkeys(store_names or []))
+        if self.union and len(names) > 1:
+            res = self._search_union(names, question, k, filt)
+            if res is not None:
+                self.last_path = "union"
+                hits = []
+                for sc, si, row, st in res:
+                    info = st.row_info(row)
+                    if info is None:
+                        continue
+                    fid, text, title, uri = info
+                    hits.append(Hit(sc, names[si], row, fid, text, title, uri))
+                return hits[:k]
+        self.last_path = "per-store"
         hits = []
-        for si, name in enumerate(store_names or []):
+        for si, name in enumerate(names):
             st = self.registry.get(name)
             if st is None or st.index.rows == 0:
                 continue

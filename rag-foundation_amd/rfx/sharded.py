@@ -50,6 +50,7 @@ class ShardedIndex:
         self.bases = [0] * len(self.shards)
         self._split = False
         self.generation = 0  # bumped whenever the shard layout changes (ShardedIvf rebuilds its lists)
+        self._screen = 0     # the two-pass scan's int8 copies (enable_screen), re-made on new shards
         self._tombs = []  # tombstoned global rows (re-applied after a re-split)
         distinct = len(set(self.devices)) == len(self.devices)
         self.comm = RcclComm.for_devices(self.devices) if distinct and len(self.devices) > 1 else None
@@ -141,6 +142,9 @@ class ShardedIndex:
         self.generation += 1
         if self._tombs:  # a copied tombstoned row is a NaN row: mark it dead in its new shard too
             self._tombstone(np.concatenate(self._tombs))
+        if self._screen:
+            for sh in new[1:]:
+                sh.enable_screen(self._screen)
 
     def add(self, vecs: torch.Tensor) -> int:
         """Append rows (writer path): they extend the last shard."""
@@ -247,6 +251,13 @@ class ShardedIndex:
             st.wait_stream(st0)
             gathered.record_stream(st)
         return [gathered] * len(self.shards)
+
+    def enable_screen(self, mode: int = 1) -> None:
+        """The exact two-pass scan on every shard (DeviceIndex.enable_screen; kept by re-splits)."""
+        with self._lock:
+            self._screen = int(mode)
+            for sh in self.shards:
+                sh.enable_screen(mode)
 
     # ---- IVF (config 5) --------------------------------------------------------------------------
     def new_ivf(self, nlist):

@@ -134,6 +134,7 @@ class LocalStore:
         self.lock = threading.RLock()
         self._stat = None
         self._masks = {}    # (version, filter key) -> device row mask
+        self._screen_on = False  # the index holds the two-pass scan's int8 copy (_maybe_screen)
         self.spec = {"kind": "flat"}
         self.ivf_meta = None  # committed {"id", "rows"} of the current centroids
         self.ivf = None       # this process's IvfIndex over the committed rows
@@ -234,6 +235,7 @@ class LocalStore:
         self.meta_bytes = self.files_bytes = self.tombs = 0
         self.version = -1
         self._masks = {}
+        self._screen_on = False
 
     def _sync(self, man=None, stat=None):
         """Catch up with the committed state on disk (caller holds self.lock).  Incremental: only
@@ -269,6 +271,7 @@ class LocalStore:
         self.version = man["version"]
         self._stat = stat
         self._ivf_catch_up()
+        self._maybe_screen()
 
     def _apply_file_record(self, r):
         if r["op"] == "add":
@@ -321,6 +324,7 @@ class LocalStore:
                 self._rollback(first)
                 raise
             self._ivf_catch_up()
+            self._maybe_screen()
             return file_id, first
 
     def _rollback(self, first):
@@ -404,6 +408,22 @@ class LocalStore:
             self.ivf, self.ivf_id = ivf, cid
         self.ivf.add_from(self.index, self.index.rows)
 
+    def _maybe_screen(self):
+        """Large bf16/f16 stores (d 768 / 1024) answer batched searches (> 64 questions) with the
+        exact two-pass scan: an int8 copy of the rows (dim bytes per row, kept current
+        by every append / tombstone inside librfx) screened on the i8 matrix cores, the survivors
+        re-scored exactly.  RFX_SCREEN=auto (default: from RFX_SCREEN_MIN_ROWS rows, 262,144) | 1
+        (always) | 0 (never).  Results are the exact scan's either way."""
+        mode = os.environ.get("RFX_SCREEN", "auto")
+        if mode == "0" or self._screen_on or not hasattr(self.index, "enable_screen"):
+            return
+        if self.dtype not in ("bf16", "f16") or self.dim not in (768, 1024) or self.index.rows == 0:
+            return
+        if mode != "1" and self.index.rows < int(os.environ.get("RFX_SCREEN_MIN_ROWS", "262144")):
+            return
+        self.index.enable_screen(1)
+        self._screen_on = True
+
     def ivf_ready(self) -> bool:
         return self.ivf is not None and self.ivf.rows == self.index.rows
 
@@ -449,9 +469,7 @@ class LocalStore:
             key = (self.version, filters.filter_key(metadata_filter))
             if key in self._masks:
                 return self._masks[key]
-            ranges = [(f["first"], f["n"]) for f in self.files.values()
-                      if not f["deleted"] and f["n"] and
-                      filters.file_matches(filters.normalize_metadata(f.get("metadata")), metadata_filter)]
+            ranges = self.mask_ranges(metadata_filter)
             mask = None
             if ranges:
                 words = filters.row_mask_words(self.index.rows, ranges)
@@ -460,6 +478,13 @@ class LocalStore:
                 self._masks.clear()
             self._masks[key] = mask
             return mask
+
+    def mask_ranges(self, metadata_filter):
+        """(first, count) row ranges of the live files whose upload metadata matches the filter."""
+        with self.lock:
+            return [(f["first"], f["n"]) for f in self.files.values()
+                    if not f["deleted"] and f["n"] and
+                    filters.file_matches(filters.normalize_metadata(f.get("metadata")), metadata_filter)]
 
     def row_info(self, row):
         """(file_id, chunk text, title, uri) of a row, or None for a row this process has no
