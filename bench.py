@@ -73,6 +73,12 @@ def parse():
     ap.add_argument("--backend", default="rccl", choices=["rccl", "gloo"])
     ap.add_argument("--one-device", action="store_true")
     ap.add_argument("--check", action="store_true")
+    # the N > 1 step (records, RCCL all-gather, gathered merge, per-phase timings) at world 1:
+    # a 1-rank RCCL communicator from librfx (rfx_comm_init_rank), so the path runs on a 1-GPU box
+    ap.add_argument("--force-comm", action="store_true")
+    # RCCL exchange of the N > 1 step: "gather" (default) = every rank's records to rank 0, where the
+    # answer is assembled (grouped send / recv, one hop); "allgather" = every rank gets all records
+    ap.add_argument("--exchange", default="gather", choices=["gather", "allgather"])
     return ap.parse_args()
 
 
@@ -139,6 +145,9 @@ def main():
     from rfx.index import DeviceIndex, merge_gathered, synth_rows
 
     comm, exchange_note = None, None
+    multi = world > 1 or a.force_comm  # the sharded step: records -> all-gather -> gathered merge
+    if world == 1 and a.force_comm:
+        comm = rdist.RcclComm.for_rank(1, 0, local, rdist.RcclComm.unique_id())
     if world > 1 and a.backend == "rccl":
         # every rank must take the same exchange: agree on RCCL's init over the gloo control plane.
         # A failed init ends the run unless --allow-host-exchange (then the JSON line says so)
@@ -184,7 +193,7 @@ def main():
     rec = torch.empty((a.nq, a.k, 2), dtype=torch.int64, device=dev)
     ws = torch.empty(max(ix.workspace_bytes(a.nq, a.k), 1), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(dev)
-    gathered = torch.empty((world, a.nq, a.k, 2), dtype=torch.int64, device=dev) if world > 1 else None
+    gathered = torch.empty((world, a.nq, a.k, 2), dtype=torch.int64, device=dev) if multi else None
     torch.cuda.synchronize()
 
     from rfx import _lib
@@ -204,7 +213,7 @@ def main():
         h = ixs[i % copies].handle
         e0 = ctypes.c_void_p(ev[0].cuda_event) if ev is not None else None
         e1 = ctypes.c_void_p(ev[1].cuda_event) if ev is not None else None
-        if world == 1:
+        if not multi:
             check(lib.rfx_search_timed(h, ptr(q), a.nq, a.k, None, 0, 0, ptr(out_s), ptr(out_r), None, ptr(ws),
                                        ws.numel(), stream_ptr(stream), e0, e1))
             if ev is not None:
@@ -216,7 +225,15 @@ def main():
         if ev is not None:
             ev[2].record(stream)
         if comm is not None:
-            comm.allgather_records([rec], [gathered], [stream])
+            if a.exchange == "gather":
+                comm.gather_records([rec], [gathered if rank == 0 else None], [stream], root=0)
+                if rank != 0:  # the answer is rank 0's: nothing to merge here
+                    if ev is not None:
+                        ev[3].record(stream)
+                        ev[4].record(stream)
+                    return None
+            else:
+                comm.allgather_records([rec], [gathered], [stream])
             g = gathered
         else:  # --one-device rehearsal / --allow-host-exchange: through host memory (gloo)
             with torch.cuda.stream(stream):
@@ -251,16 +268,17 @@ def main():
 
     scan_ms = avg(0, 1)
     phases = {"scan_ms": scan_ms, "search_done_ms": avg(0, 2)}
+    if multi:
+        phases.update({"records_merge_ms": avg(1, 2), "exchange_ms": avg(2, 3), "gathered_merge_ms": avg(3, 4)})
     if world > 1:
-        phases.update({"records_merge_ms": avg(1, 2), "allgather_ms": avg(2, 3), "gathered_merge_ms": avg(3, 4)})
         t = torch.tensor([elapsed] + list(phases.values()), dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t[0])
         phases = {k_: float(v) for k_, v in zip(phases, t[1:].tolist())}
         scan_ms = phases["scan_ms"]
     if a.check:  # the global top-k of the last step equals one whole-index search (exact)
-        got_s, got_r = out
         if rank == 0:
+            got_s, got_r = out
             full = DeviceIndex(a.dim, a.dtype, local, capacity=a.rows)
             full.add_synthetic(a.seed, a.rows)
             ref_s, ref_r = full.search(q, a.k)
@@ -304,7 +322,9 @@ def main():
                                f"GPU(s), {a.nq} queries/batch, brute-force top-{a.k}",
                    "rows": a.rows, "dim": a.dim, "nq": a.nq, "k": a.k, "parallelism": f"rowshard{world}",
                    "corpus_copies": copies, "scan": a.scan,
-                   "exchange": ("RCCL all-gather from librfx (rfx_allgather_records)" if comm is not None else
+                   "exchange": (("RCCL gather to rank 0 from librfx (rfx_gather_records: grouped send/recv)"
+                                 if a.exchange == "gather" else "RCCL all-gather from librfx (rfx_allgather_records)")
+                                if comm is not None else
                                 exchange_note if exchange_note else
                                 "host (gloo) rehearsal" if world > 1 else "none (one shard)"),
                    "scan_kernel": SCAN_NAMES[kern]},

@@ -227,6 +227,13 @@ int rfx_comm_info(rfx_comm_t c, int* world, int* rank, int* n_local);
 int rfx_comm_destroy(rfx_comm_t c);
 int rfx_allgather_records(rfx_comm_t c, const void* const* sends_d, void* const* recvs_d, int64_t nq, int k,
                           void* const* streams);
+/* rfx_gather_records: the records of every rank to ONE rank (`root`), where the answer is assembled:
+ * one grouped ncclSend per rank to the root and world ncclRecv on the root (one hop over xGMI's
+ * point-to-point links instead of an all-gather ring's world - 1).  sends_d[i] as above;
+ * recvs_d[i] = [world][nq][k] records for the local device that IS the root (rank mode: the
+ * caller's device when rank == root; group mode: local device index root), NULL elsewhere. */
+int rfx_gather_records(rfx_comm_t c, const void* const* sends_d, void* const* recvs_d, int root, int64_t nq,
+                       int k, void* const* streams);
 
 /* ---- text → features (host) ---------------------------------------------------------------
  * The reference has no chunker/tokeniser of its own (chunking_config is forwarded to Gemini,

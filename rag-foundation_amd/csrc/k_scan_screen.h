@@ -17,8 +17,9 @@
 // Let a_k be the k-th best A over live rows.  The k rows that reach it have exact scores
 // >= a_k − E_q, so the true k-th best exact score is too, and a row of the true top-k has
 // A >= a_k − 2 E_q / s_y = a_k − e2.  The kernel keeps every such row:
-//   * pruning.  Kernel 6's bound (own list's KL-th best, the cross-workgroup slot table) is a lower
-//     bound of a_k (KL >= k); a row is looked at only when A >= bound − e2;
+//   * pruning.  The bound max(own list's KL-th best, KL-th largest of the query's 16 cross-workgroup
+//     slots; tau_kth below) is a lower bound of a_k (KL >= k); a row is looked at only when
+//     A >= bound − e2;
 //   * lists.  Each lane keeps the KL best A of the rows it looked at (LDS, as kernel 6) and the
 //     best A it had to drop (`drop`: not inserted, or evicted).  k_screen.hip's select kernel
 //     finds a_k from the lists' union, and takes the fallback (the exact kernel on the whole
@@ -52,7 +53,7 @@ constexpr int kSlot = kTM * kRowB;        // 8 KB: 32 rows × 256 codes
 #endif
 constexpr int kRing = RFX_K10_RING;       // slots; RING - 1 stages in flight
 constexpr int kGPW = 1;                   // LDS-DMA pieces per wave per stage (8 KB / 1 KB / 8 waves)
-constexpr int kTauW = 16;                 // u32 per query in the threshold table (KL <= 10 used)
+constexpr int kTauW = 16;                 // u32 per query in the threshold table: 16 slots (tau_kth)
 constexpr int kTauBytes = kQG * kTauW * 4;  // 16 KB
 constexpr int kTauGPW = kTauBytes / 1024 / kWaves;
 constexpr int kMR = 8;  // tile-metadata slots (1 KB each: 64 lane copies of the 16-B record)
@@ -68,6 +69,44 @@ static_assert(lds_bytes<10, 12>() <= 163840, "LDS budget");
 static_assert(kSlot / 1024 == kWaves * kGPW && kTauGPW == 2, "DMA pieces per wave");
 
 __device__ __forceinline__ bool tau_refresh_tile(int it) { return it < 2 || (it & 3) == 3; }
+
+// The pruning bound from a query's kTauW = 16 slots: list j publishes its best A to slot j % 16, so
+// the slots hold the A of 16 distinct rows (lists are disjoint row sets) and the KL-th largest slot is
+// a lower bound of the query's KL-th best A.  Against kernel 6's min over KL slots it sits much closer
+// to the KL-th best (simulated on 10M Gaussian scores, 512 lists: 14.6 rows above the bound against
+// 26.2 for k = 10), so fewer rows reach bound - e2 and fewer tiles take the slow path.  Bitonic sort of
+// the 16 values, descending (80 compare-exchanges; the refresh runs every 4th tile).
+template <int KL>
+__device__ __forceinline__ uint32_t kth16(uint32_t (&v)[16]) {
+#pragma unroll
+  for (int k = 2; k <= 16; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int l = i ^ j;
+        if (l > i) {
+          const uint32_t a = v[i], b = v[l];
+          const bool desc = (i & k) == 0;
+          v[i] = desc ? max(a, b) : min(a, b);
+          v[l] = desc ? min(a, b) : max(a, b);
+        }
+      }
+  return v[KL - 1];
+}
+template <int KL>
+__device__ __forceinline__ uint32_t tau_kth(const uint8_t* p) {
+  uint32_t v[16];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint4 a = *(const uint4*)(p + 16 * i);
+    v[4 * i] = a.x;
+    v[4 * i + 1] = a.y;
+    v[4 * i + 2] = a.z;
+    v[4 * i + 3] = a.w;
+  }
+  return kth16<KL>(v);
+}
 
 __device__ __forceinline__ v4i32 mfma_i8(const uint4& a, const uint4& b, const v4i32& c) {
   return __builtin_amdgcn_mfma_i32_16x16x64_i8(__builtin_bit_cast(v4i32, a), __builtin_bit_cast(v4i32, b), c, 0, 0, 0);
@@ -126,7 +165,8 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
 // fragments prefetched 2 k-steps ahead (d 768 only), 8 = no corpus stream after the prologue (MFMA +
 // LDS only; wrong scores, timing only), 32 = count slow-path entries (threshold slot 15 of each
 // wave's first query), 64 = the fast path on the store-wide integer bound (max tile scale) instead
-// of the tile's own scale, 128 = the epilogue in place at each tile's end (no alternating accumulators).
+// of the tile's own scale, 128 = the epilogue in place at each tile's end (no alternating accumulators),
+// 256 = kernel 6's slot-table bound (min over KL slots) instead of the KL-th largest of 16.
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
@@ -243,7 +283,10 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
     }
   };
   const bool odd = ((lane >> 4) & 1) != 0;
-  const uint32_t slot_voff = (uint32_t)(q * kTauW + lst % KL) * 4u;
+  // MODE 32 (debug) counts slow-path entries in slot 15 of each wave's first query: 15 slots then;
+  // MODE 256 (debug): kernel 6's bound, the min over KL slots (list j -> slot j % KL)
+  constexpr int kSlots = (MODE & 256) != 0 ? KL : (MODE & 32) != 0 ? kTauW - 1 : kTauW;
+  const uint32_t slot_voff = (uint32_t)(q * kTauW + lst % kSlots) * 4u;
   const uint8_t* const tq = lds + kTauOff + (w * kQW + (lane & 15) + 16 * ((lane >> 4) & 1)) * (kTauW * 4);
   // A fragment of row block rb, k-step kk of a slot: row 16 rb + (lane & 15), chunk 4 kk + (lane >> 4)
   const uint8_t* const frag_base = lds + (lane & 15) * kRowB;
@@ -334,7 +377,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   auto tile_body = [&](const int it, v4i32(&acc4)[4], v4i32(&accp)[4], const bool prev) {
     const int gbase = it * NST;
     if (it >= 2 && tau_refresh_tile(it - 2)) {
-      thr = max(thr, tau_min<KL>(tq));
+      thr = max(thr, (MODE & 256) != 0 ? tau_min<KL>(tq) : tau_kth<KL>(tq));
       set_bounds();
     }
     // metadata records younger than stage g+1's piece at stage s's wait: stages h in g+1 .. g+RING-1
@@ -421,10 +464,17 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (q < nq) {
     // entries below (the query's bound as it stands now) − e2 cannot be survivors: dropped here
-    uint32_t m = 0xffffffffu;
+    uint32_t sl[16];
 #pragma unroll
-    for (int j = 0; j < KL; ++j)
-      m = min(m, __hip_atomic_load(tau + (int64_t)q * kTauW + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    for (int j = 0; j < 16; ++j)
+      sl[j] = j >= kSlots ? 0u : __hip_atomic_load(tau + (int64_t)q * kTauW + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t m = kth16<KL>(sl);
+    if constexpr ((MODE & 256) != 0) {
+      m = 0xffffffffu;
+#pragma unroll
+      for (int j = 0; j < KL; ++j)
+        m = min(m, __hip_atomic_load(tau + (int64_t)q * kTauW + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
     const uint32_t fin = max(thr, m);
     const float lo = fin ? unord(fin) - e2 : -__builtin_inff();
     const int64_t o = ((int64_t)q * n_lists + lst) * KL;

@@ -131,6 +131,14 @@ int fused_state(Index& ix, hipStream_t st, uint32_t** out) {
     *out = it->second;
     return RFX_OK;
   }
+  // bounded: callers that make a stream per request would grow the map forever.  Past 64
+  // streams every launch is drained (a launch leaves its state zeroed when it completes), then all
+  // states are freed; the streams that search again get fresh ones.
+  if (ix.fused_state.size() >= 64) {
+    RFX_HIP(hipDeviceSynchronize());
+    for (auto& kv : ix.fused_state) RFX_HIP(hipFree(kv.second));
+    ix.fused_state.clear();
+  }
   uint32_t* p = nullptr;
   const size_t bytes = (size_t)rfx::kValuFusedStateWords * 4;
   if (hipMalloc(&p, bytes) != hipSuccess) return fail(RFX_ENOMEM, "hipMalloc(%zu) failed (search state)", bytes);

@@ -9,7 +9,9 @@
 //   * one index-server process owning several GPUs: rfx_comm_init_all (ncclCommInitAll), and the
 //     all-gather runs as one RCCL group over the process's devices.
 // The payload is tiny (nq·k·16 B per rank: 40 KB at nq 256, k 10), so the collective is latency-
-// bound over xGMI; one ncclAllGather per batch, no bucketing.
+// bound over xGMI; one ncclAllGather per batch, no bucketing — or, where only one rank assembles the
+// answer (the query's front end), rfx_gather_records: grouped ncclSend / ncclRecv to that rank, one
+// hop over the point-to-point links.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -151,6 +153,47 @@ int rfx_allgather_records(rfx_comm_t h, const void* const* sends_d, void* const*
     const ncclResult_t r = ncclGroupEnd();
     if (r != ncclSuccess && rc == RFX_OK) rc = rfx::api_fail(RFX_EDEVICE, "ncclGroupEnd: %s", ncclGetErrorString(r));
   }
+  (void)hipSetDevice(prev);
+  return rc;
+}
+
+int rfx_gather_records(rfx_comm_t h, const void* const* sends_d, void* const* recvs_d, int root, int64_t nq, int k,
+                       void* const* streams) {
+  auto c = get(h);
+  if (!c) return rfx::api_fail(RFX_EINVAL, "unknown communicator");
+  if (nq < 0 || k < 1 || k > 64) return rfx::api_fail(RFX_EINVAL, "nq %lld, k %d", (long long)nq, k);
+  if (root < 0 || root >= c->world) return rfx::api_fail(RFX_EINVAL, "root %d of world %d", root, c->world);
+  if (!sends_d || !recvs_d || !streams) return rfx::api_fail(RFX_EINVAL, "null buffer arrays");
+  const size_t bytes = (size_t)nq * k * 16;
+  if (bytes == 0) return RFX_OK;
+  const int n = (int)c->comms.size();
+  // the local index of the root (group mode: device index root; rank mode: 0 when this rank is root)
+  const int lroot = c->group ? root : (c->rank == root ? 0 : -1);
+  for (int i = 0; i < n; ++i)
+    if (!sends_d[i] || (i == lroot && !recvs_d[i]))
+      return rfx::api_fail(RFX_EINVAL, "null buffer for local device %d", i);
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) return rfx::api_fail(RFX_EDEVICE, "hipGetDevice");
+  std::lock_guard<std::mutex> lk(c->mu);
+  RFX_NCCL(ncclGroupStart());
+  int rc = RFX_OK;
+  for (int i = 0; i < n && rc == RFX_OK; ++i) {
+    if (hipSetDevice(c->devices[i]) != hipSuccess) {
+      rc = rfx::api_fail(RFX_EDEVICE, "hipSetDevice(%d)", c->devices[i]);
+      break;
+    }
+    hipStream_t st = (hipStream_t)streams[i];
+    if (i == lroot)
+      for (int p = 0; p < c->world && rc == RFX_OK; ++p) {
+        const ncclResult_t r = ncclRecv((uint8_t*)recvs_d[i] + (size_t)p * bytes, bytes, ncclUint8, p, c->comms[i], st);
+        if (r != ncclSuccess) rc = rfx::api_fail(RFX_EDEVICE, "ncclRecv from %d: %s", p, ncclGetErrorString(r));
+      }
+    if (rc != RFX_OK) break;
+    const ncclResult_t r = ncclSend(sends_d[i], bytes, ncclUint8, root, c->comms[i], st);
+    if (r != ncclSuccess) rc = rfx::api_fail(RFX_EDEVICE, "ncclSend: %s", ncclGetErrorString(r));
+  }
+  const ncclResult_t r = ncclGroupEnd();
+  if (r != ncclSuccess && rc == RFX_OK) rc = rfx::api_fail(RFX_EDEVICE, "ncclGroupEnd: %s", ncclGetErrorString(r));
   (void)hipSetDevice(prev);
   return rc;
 }

@@ -112,6 +112,7 @@ SIGNATURES = {
     "rfx_comm_info": ([_u64, _pi, _pi, _pi], _i),
     "rfx_comm_destroy": ([_u64], _i),
     "rfx_allgather_records": ([_u64, _p, _p, _i64, _i, _p], _i),
+    "rfx_gather_records": ([_u64, _p, _p, _i, _i64, _i, _p], _i),
     "rfx_search_workspace_bytes": ([_u64, _i64, _i, _psz], _i),
     "rfx_search": ([_u64, _p, _i64, _i, _p, _p, _p, _sz, _p], _i),
     "rfx_scan_plan": ([_u64, _i64, _i, _pi, _pi64], _i),

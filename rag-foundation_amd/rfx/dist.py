@@ -100,6 +100,25 @@ class RcclComm:
         stp = (ctypes.c_void_p * n)(*[st.cuda_stream for st in streams])
         check(lib.rfx_allgather_records(self.handle, sp, rp, nq, k, stp))
 
+    def gather_records(self, sends, recvs, streams, root: int = 0):
+        """sends[i]: [nq][k][2] int64 records on local device i; recvs[i]: [world][nq][k][2] on the
+        local device that is `root` (None elsewhere): grouped send / recv to one rank."""
+        n = self.n_local
+        if not (len(sends) == len(recvs) == len(streams) == n):
+            raise ValueError(f"need {n} send/recv/stream entries")
+        nq, k = sends[0].shape[0], sends[0].shape[1]
+        lroot = root if self.n_local > 1 else (0 if self.rank == root else -1)
+        for i, (s, r) in enumerate(zip(sends, recvs)):
+            if s.shape != (nq, k, 2) or s.dtype != torch.int64 or not s.is_contiguous():
+                raise ValueError("records must be contiguous int64 [nq][k][2]")
+            if i == lroot and (r is None or r.shape != (self.world, nq, k, 2) or r.dtype != torch.int64
+                               or not r.is_contiguous()):
+                raise ValueError("the root's receive buffer must be contiguous int64 [world][nq][k][2]")
+        sp = (ctypes.c_void_p * n)(*[s.data_ptr() for s in sends])
+        rp = (ctypes.c_void_p * n)(*[r.data_ptr() if r is not None else None for r in recvs])
+        stp = (ctypes.c_void_p * n)(*[st.cuda_stream for st in streams])
+        check(lib.rfx_gather_records(self.handle, sp, rp, int(root), nq, k, stp))
+
     def close(self):
         if getattr(self, "handle", None):
             check(lib.rfx_comm_destroy(self.handle))

@@ -232,13 +232,18 @@ class ShardedIndex:
         shard's stream).  Distinct devices: one RCCL all-gather; logical shards: a stack on stream 0."""
         st0 = self._streams[0]
         if self.comm is not None:
+            if not everywhere:  # the answer is assembled on device 0: one hop (rfx_gather_records)
+                o = torch.empty((len(self.devices), nq, k, 2), dtype=torch.int64, device=torch.device("cuda", self.devices[0]))
+                o.record_stream(st0)
+                self.comm.gather_records(recs, [o] + [None] * (len(self.devices) - 1), self._streams, root=0)
+                return [o]
             outs = []
             for d, st in zip(self.devices, self._streams):
                 o = torch.empty((len(self.devices), nq, k, 2), dtype=torch.int64, device=torch.device("cuda", d))
                 o.record_stream(st)
                 outs.append(o)
             self.comm.allgather_records(recs, outs, self._streams)
-            return outs if everywhere else outs[:1]
+            return outs
         for st in self._streams[1:]:
             st0.wait_stream(st)
         with torch.cuda.stream(st0):

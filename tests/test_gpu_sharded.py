@@ -198,3 +198,25 @@ def test_sharded_ivf_store_equals_unsharded(tmp_path):
     assert shard.ivf_ready() and plain.ivf_ready()
     for k in (5, 10):
         same(k)
+
+
+def test_rccl_gather_records_one_rank():
+    """rfx_gather_records (grouped send/recv to the root) in both process models, world 1."""
+    from rfx.dist import RcclComm
+
+    rec = _records(256, 10, 3)
+    st = torch.cuda.current_stream()
+    comm = RcclComm.for_rank(1, 0, 0, RcclComm.unique_id())
+    out = torch.zeros((1, 256, 10, 2), dtype=torch.int64, device="cuda")
+    comm.gather_records([rec], [out], [st], root=0)
+    torch.cuda.synchronize()
+    assert torch.equal(out[0], rec)
+    with pytest.raises(ValueError):
+        comm.gather_records([rec], [None], [st], root=0)  # the root needs a receive buffer
+    comm.close()
+    comm = RcclComm.for_devices([0])
+    out = torch.zeros((1, 256, 10, 2), dtype=torch.int64, device="cuda")
+    comm.gather_records([rec], [out], [st], root=0)
+    torch.cuda.synchronize()
+    assert torch.equal(out[0], rec)
+    comm.close()
