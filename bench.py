@@ -106,11 +106,13 @@ def cpu_model():
 
 KERNEL_NAMES = {0: "scan_valu_kernel", 1: "scan_mfma_kernel", 2: "scan_mfma2_kernel", 3: "scan_mfma3_kernel",
                 4: "scan_mfma4_kernel", 5: "scan_mfma5_kernel", 6: "scan_mfma6_kernel",
-                7: "scan_mfma7_kernel", 8: "scan_mfma8_kernel", 9: "scan_mfma9_kernel", 10: "scan_screen_kernel"}
+                7: "scan_mfma7_kernel", 8: "scan_mfma8_kernel", 9: "scan_mfma9_kernel", 10: "scan_screen_kernel",
+                11: "screen_valu_kernel"}
 SCAN_NAMES = {0: "valu", 1: "mfma128", 2: "mfma256", 3: "mfma_qstationary128", 4: "mfma_qstationary256",
               5: "mfma_qstationary256_2wps", 6: "mfma16_qstationary256_2wps", 7: "mfma16_qstationary128_2wps_xcdpair",
               8: "mfma16_qstationary128_ksplit_pairs_xcdpair", 9: "mfma_f32_qstationary128",
-              10: "two_pass: i8 mfma16x16x64 screen (qstationary256_2wps) + exact re-score + gated exact fallback"}
+              10: "two_pass: i8 mfma16x16x64 screen (qstationary256_2wps) + exact re-score + gated exact fallback",
+              11: "two_pass_valu: i8 dot4 screen + exact re-score + merge in one launch, gated exact one-launch fallback"}
 
 
 def load_pmc_traffic(workload_key, kernel_name):
@@ -172,10 +174,14 @@ def main():
     r0, r1 = rdist.shard_range(a.rows, rank, world)
     n_local = r1 - r0
     esz = {"bf16": 2, "f16": 2, "f32": 4}[a.dtype]
-    copies = a.copies or min(8, max(1, -(-(768 << 20) // max(n_local * a.dim * esz, 1)) + 1))
-    if copies > 1 and n_local * a.dim * esz > (1 << 30):
+    copies = a.copies or min(8, max(1, -(-(768 << 20) // max(n_local * row_bytes, 1)) + 1))
+    if copies > 1 and n_local * row_bytes > (1 << 30):
         copies = 1  # far beyond the Infinity Cache already
-    screen = a.scan == "auto" and a.dtype in ("bf16", "f16") and a.dim in (768, 1024) and a.nq > 64 and a.k <= 10
+    # the exact two-pass scan: kernel 10 for batches (bf16/f16, nq > 64, k <= 10), kernel 11 for a few
+    # questions (any dtype, nq <= 8, 5 <= k <= 16; config 2)
+    screen = a.scan == "auto" and a.dim in (768, 1024) and (
+        (a.dtype in ("bf16", "f16") and a.nq > 64 and a.k <= 10) or (a.nq <= 8 and 5 <= a.k <= 16))
+    row_bytes = a.dim if screen else a.dim * esz  # what a scan streams per row
     ixs, build_s = [], 0.0
     for _ in range(copies):
         c = DeviceIndex(a.dim, a.dtype, local, capacity=n_local)
@@ -300,6 +306,13 @@ def main():
         kl = 4 if a.k <= 4 else 10
         alg_bytes = (n_max * a.dim + (-(-n_max // 32)) * 16 + nq_pad * a.dim + nq_pad * 4
                      + a.nq * n_lists * (kl * 8 + 4))
+    elif kern == 11:
+        # int8 codes + tile records + the raw queries + the per-block candidate lists (16 x (f32, i32))
+        # written and read back by the last block + the results (re-scored rows: a few per query)
+        rpw = -(-max(16, -(-n_max // 1024)) // 4) * 4  # plan_scan_valu: rows per wave, 4 waves per block
+        n_lists = -(-(-(-n_max // rpw)) // 4)
+        alg_bytes = (n_max * a.dim + (-(-n_max // 32)) * 16 + a.nq * a.dim * esz + 2 * a.nq * n_lists * 16 * 8
+                     + a.nq * a.k * 12)
     else:
         alg_bytes = n_max * a.dim * esz + a.nq * a.dim * esz + a.nq * a.k * 12
     achieved = alg_bytes / (scan_ms * 1e-3) / 1e9

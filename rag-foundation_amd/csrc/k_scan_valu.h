@@ -100,6 +100,8 @@ struct FusedOut {
   int k_out;
   float* out_s;
   int64_t* out_r;
+  // the two-pass scan's fallback (k_screen_valu.hip): run only when the screen set this word
+  const uint32_t* gate = nullptr;
 };
 
 template <int DT>
@@ -124,6 +126,8 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
                                                         int* __restrict__ cand_r, int n_lists,
                                                         const uint32_t* __restrict__ mask,
                                                         uint32_t* __restrict__ tau, FusedOut fo) {
+  if constexpr (FUSED)  // gated (the two-pass scan's fallback): the whole grid returns together
+    if (fo.gate && __hip_atomic_load(fo.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
   constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
   constexpr int EPV = 16 / ESZ;
   extern __shared__ __attribute__((aligned(16))) float q_lds[];  // [NQT][D]

@@ -128,10 +128,10 @@ int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dty
 
 int launch_search_valu_fused(const ValuPlan& p, const void* X, int nrows, int D, int dtype, const void* Q, int nq,
                              float* cs, int* cr, uint32_t* state, int k, float* out_s, int64_t* out_r,
-                             hipStream_t st, const uint32_t* mask) {
+                             hipStream_t st, const uint32_t* mask, const uint32_t* gate) {
   // state: [kFusedMaxNq] bounds then [q_slices] counters, all zero (and left zero)
   return launch_valu(p, X, nrows, D, dtype, Q, nq, cs, cr, st, mask, state,
-                     FusedOut{state + kValuFusedMaxNq, k, out_s, out_r});
+                     FusedOut{state + kValuFusedMaxNq, k, out_s, out_r, gate});
 }
 
 // Diagnostic streaming read (HBM ceiling calibration): every byte read once with dwordx4.

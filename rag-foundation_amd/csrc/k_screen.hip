@@ -57,8 +57,24 @@ __device__ __forceinline__ int8_t code_of(float x, float s) {
 // rows (0 for a tile without any), c = clamp(rint(x / s_t), ±127).  stats[0] / stats[1] grow to the
 // max over live rows of ||x|| and ||x − s_t c|| (f64 sums, rounded up to f32, atomicMax on the bits),
 // stats[2] to the max tile scale.
+// 8 consecutive stored elements from element index i (16-B aligned groups), widened exactly
+template <int DT>
+__device__ __forceinline__ void load8(const void* X, int64_t i, float (&f)[8]) {
+  if constexpr (DT == RFX_F32) {
+    const uint4 a = *(const uint4*)((const float*)X + i), b = *(const uint4*)((const float*)X + i + 4);
+    const uint32_t u[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = __uint_as_float(u[e]);
+  } else {
+    const uint4 v = *(const uint4*)((const uint16_t*)X + i);
+    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = widen<DT>((uint16_t)(e & 1 ? u[e >> 1] >> 16 : u[e >> 1] & 0xffffu));
+  }
+}
+
 template <int DT, int D>
-__global__ __launch_bounds__(256) void screen_quantize_kernel(const uint16_t* __restrict__ X, int64_t tile0,
+__global__ __launch_bounds__(256) void screen_quantize_kernel(const void* __restrict__ X, int64_t tile0,
                                                               const int64_t* __restrict__ tiles,
                                                               int8_t* __restrict__ codes, uint4* __restrict__ tmeta,
                                                               uint32_t* __restrict__ stats) {
@@ -66,7 +82,7 @@ __global__ __launch_bounds__(256) void screen_quantize_kernel(const uint16_t* __
   const int64_t tile = tiles ? tiles[blockIdx.x] : tile0 + blockIdx.x;
   const int t = threadIdx.x, row = t >> 3, seg = t & 7;
   const int64_t r = tile * 32 + row;
-  const uint16_t* xr = X + r * D + seg * PER;
+  const int64_t xr = r * D + seg * PER;  // element index of the thread's segment
   __shared__ float wmax[4];
   __shared__ uint32_t word;
   if (t == 0) word = 0u;
@@ -74,11 +90,11 @@ __global__ __launch_bounds__(256) void screen_quantize_kernel(const uint16_t* __
   float am = 0.f;
 #pragma unroll 4
   for (int i = 0; i < PER; i += 8) {
-    const uint4 v = *(const uint4*)(xr + i);
-    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+    float fv[8];
+    load8<DT>(X, xr + i, fv);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float f = widen<DT>((uint16_t)(e & 1 ? u[e >> 1] >> 16 : u[e >> 1] & 0xffffu));
+      const float f = fv[e];
       nan |= f != f;
       am = fmaxf(am, fabsf(f));
     }
@@ -99,12 +115,12 @@ __global__ __launch_bounds__(256) void screen_quantize_kernel(const uint16_t* __
   int8_t* cw = codes + r * D + seg * PER;
 #pragma unroll 4
   for (int i = 0; i < PER; i += 8) {
-    const uint4 v = *(const uint4*)(xr + i);
-    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+    float fv[8];
+    load8<DT>(X, xr + i, fv);
     uint32_t pk[2] = {0u, 0u};
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float f = widen<DT>((uint16_t)(e & 1 ? u[e >> 1] >> 16 : u[e >> 1] & 0xffffu));
+      const float f = fv[e];
       const int8_t c = (!dead && s > 0.f) ? code_of(f, s) : (int8_t)0;
       pk[e >> 2] |= (uint32_t)(uint8_t)c << (8 * (e & 3));
       if (!dead) {
@@ -354,18 +370,26 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
 }  // namespace
 
 // ---- host launchers --------------------------------------------------------------------------------
-bool screen_supported(int D, int dtype) { return (D == 768 || D == 1024) && (dtype == RFX_BF16 || dtype == RFX_F16); }
+// the int8 copy: bf16 / f16 / f32 stores at d 768 / 1024 (kernel 10 screens bf16 / f16 batches,
+// kernel 11 a few questions of any of the three)
+bool screen_supported(int D, int dtype) {
+  return (D == 768 || D == 1024) && (dtype == RFX_BF16 || dtype == RFX_F16 || dtype == RFX_F32);
+}
 
 void launch_screen_quantize(const void* X, int D, int dtype, int64_t tile0, int64_t ntiles, const int64_t* tiles_d,
                             int8_t* codes, void* tmeta, uint32_t* stats, hipStream_t st) {
   if (ntiles <= 0) return;
 #define RFX_SQ(DTV, DV)                                                                                         \
-  hipLaunchKernelGGL((screen_quantize_kernel<DTV, DV>), dim3((unsigned)ntiles), dim3(256), 0, st, (const uint16_t*)X, \
+  hipLaunchKernelGGL((screen_quantize_kernel<DTV, DV>), dim3((unsigned)ntiles), dim3(256), 0, st, X, \
                      tile0, tiles_d, codes, (uint4*)tmeta, stats)
   if (dtype == RFX_BF16 && D == 768)
     RFX_SQ(RFX_BF16, 768);
   else if (dtype == RFX_BF16)
     RFX_SQ(RFX_BF16, 1024);
+  else if (dtype == RFX_F32 && D == 768)
+    RFX_SQ(RFX_F32, 768);
+  else if (dtype == RFX_F32)
+    RFX_SQ(RFX_F32, 1024);
   else if (D == 768)
     RFX_SQ(RFX_F16, 768);
   else

@@ -473,6 +473,13 @@ int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t
   return RFX_OK;
 }
 
+// Kernel 11 (k_screen_valu.hip): a few questions (nq <= 8) on an index holding the int8 copy, on a
+// VALU plan with lists of 16 (5 <= k <= 16) — one launch, plus the gated exact one-launch search.
+bool screen_valu_eligible(const Index& ix, const SearchLayout& L, int64_t nq, int k) {
+  return ix.screen && ix.rows > 0 && L.kernel == 0 && nq >= 1 && nq <= 8 && k <= 16 && L.vp.k_slot == 16 &&
+         rfx::screen_supported(ix.dim, ix.dtype) && fused_enabled();
+}
+
 }  // namespace
 
 namespace rfx {
@@ -1144,6 +1151,23 @@ int search_impl(rfx_index_t h, const void* queries_d, int64_t nq, int k, const u
   if (nq == 0) return RFX_OK;
   float* cs = (float*)(ws + L.cs_off);
   int32_t* cr = (int32_t*)(ws + L.cr_off);
+  if (!out_rec && row_offset == 0 && screen_valu_eligible(*ix, L, nq, k) && ((uintptr_t)queries_d & 15) == 0) {
+    uint32_t* state = nullptr;
+    if ((rc = fused_state(*ix, st, &state))) return rc;
+    uint32_t* sv = state + rfx::kScreenValuState;
+    if ((rc = mark(ev0))) return rc;
+    if (rfx::launch_screen_valu(L.vp, ix->scodes, ix->smeta, ix->sstats, (int)ix->rows, ix->dim, ix->dtype, ix->data,
+                                queries_d, (int)nq, row_mask_d, sv, cs, cr, k, out_scores_d, out_rows_d,
+                                ix->screen == 2, st) != 0)
+      return fail(RFX_EUNSUPPORTED, "two-pass VALU search launch rejected");
+    if ((rc = mark(ev1))) return rc;
+    // the exact one-launch search, gated on the word the screen's last block wrote
+    if (rfx::launch_search_valu_fused(L.vp, ix->data, (int)ix->rows, ix->dim, ix->dtype, queries_d, (int)nq, cs, cr,
+                                      state, k, out_scores_d, out_rows_d, st, row_mask_d, sv + 24) != 0)
+      return fail(RFX_EUNSUPPORTED, "VALU search launch rejected");
+    RFX_HIP(hipGetLastError());
+    return RFX_OK;
+  }
   // (the one-launch kernel reads the caller's queries with 16-B loads: an unaligned buffer takes
   // the three-launch path, whose widening copy is aligned)
   if (!out_rec && row_offset == 0 && L.kernel == 0 && ix->rows > 0 && nq <= rfx::kValuFusedMaxNq && fused_enabled() &&
@@ -1209,7 +1233,7 @@ int rfx_search_plan(rfx_index_t h, int64_t nq, int k, int* out_kernel) {
   SearchLayout L;
   int rc = make_search_layout(*ix, nq, k, L);
   if (rc) return rc;
-  *out_kernel = L.kernel;
+  *out_kernel = screen_valu_eligible(*ix, L, nq, k) ? 11 : L.kernel;
   return RFX_OK;
 }
 
@@ -1219,7 +1243,7 @@ int rfx_index_screen(rfx_index_t h, int mode, void* stream) {
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
   if (mode < 0 || mode > 2) return fail(RFX_EINVAL, "screen mode %d (0 off, 1 on, 2 on + forced fallback)", mode);
   if (mode && !rfx::screen_supported(ix->dim, ix->dtype))
-    return fail(RFX_EUNSUPPORTED, "the two-pass scan needs a bf16/f16 index of dim 768 or 1024 (dim=%d dtype=%d)",
+    return fail(RFX_EUNSUPPORTED, "the two-pass scan needs an index of dim 768 or 1024 (dim=%d dtype=%d)",
                 ix->dim, ix->dtype);
   hipStream_t st = (hipStream_t)stream;
   RFX_WLOCK(ix);

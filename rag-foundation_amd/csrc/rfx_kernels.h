@@ -37,10 +37,20 @@ int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dty
 // p.q_slices arrival counters, ALL ZERO on entry — the kernel leaves them zero again, so a state
 // buffer zeroed once serves every later search on one stream (rfx_api.hip keeps one per stream).
 constexpr int kValuFusedMaxNq = 1024;
-constexpr int kValuFusedStateWords = kValuFusedMaxNq + 1024;
+// + 32 words for the lone-question two-pass scan (kernel 11): counter, bounds, drops, fallback gate
+constexpr int kScreenValuState = kValuFusedMaxNq + 1024;
+constexpr int kValuFusedStateWords = kScreenValuState + 32;
+// gate (optional): the launch runs only when *gate != 0 (the two-pass scan's fallback)
 int launch_search_valu_fused(const ValuPlan& p, const void* X, int nrows, int D, int dtype, const void* Q, int nq,
                              float* cs, int* cr, uint32_t* state, int k, float* out_s, int64_t* out_r,
-                             hipStream_t st, const uint32_t* mask = nullptr);
+                             hipStream_t st, const uint32_t* mask = nullptr, const uint32_t* gate = nullptr);
+// Kernel 11 (k_screen_valu.hip): the exact two-pass scan of nq <= 8 questions in one launch over the
+// index's int8 copy (codes X8, tile records tmeta, quantiser stats), the exact rows X / queries Q in
+// the index dtype; writes (out_s, out_r) and the fallback gate state[24] (state = the index's
+// per-stream search state + kScreenValuState, zero on entry and left zero except the gate).
+int launch_screen_valu(const ValuPlan& p, const int8_t* X8, const void* tmeta, const uint32_t* stats, int nrows, int D,
+                       int dtype, const void* X, const void* Q, int nq, const uint32_t* mask, uint32_t* state,
+                       float* cs, int* cr, int k, float* out_s, int64_t* out_r, int force, hipStream_t st);
 
 // ---- MFMA scan (batched bf16 / f16) -------------------------------------------------------
 struct MfmaPlan {

@@ -200,14 +200,16 @@ class DeviceIndex:
 
     # ---- the exact two-pass scan (int8 copy of the store) --------------------------------
     def enable_screen(self, mode: int = 1, stream=None) -> None:
-        """Keep an int8 copy of the rows (dim bytes per row) and answer batched searches with the
-        exact two-pass scan: int8 screen, exact re-score of the survivors, the exact scan as a gated
-        fallback.  mode 0 drops the copy; mode 2 forces the fallback (tests)."""
+        """Keep an int8 copy of the rows (dim bytes per row) and answer searches with the exact
+        two-pass scan where it applies (kernel 10: bf16/f16 batches of > 64 questions; kernel 11: up
+        to 8 questions of any dtype): int8 screen, exact re-score of the survivors, the exact scan as
+        a gated fallback.  mode 0 drops the copy; mode 2 forces the fallback (tests)."""
         with torch.cuda.device(self.device):
             check(lib.rfx_index_screen(self.handle, int(mode), stream_ptr(stream)))
 
     def search_plan(self, nq: int, k: int) -> int:
-        """Kernel rfx_search runs for (nq, k): 10 = the two-pass scan."""
+        """Kernel rfx_search runs for (nq, k): 10 = the two-pass scan of a batch (int8 MFMA screen),
+        11 = the two-pass scan of up to 8 questions (int8 dot4 screen, one launch)."""
         kern = ctypes.c_int()
         check(lib.rfx_search_plan(self.handle, int(nq), int(k), ctypes.byref(kern)))
         return kern.value

@@ -409,17 +409,18 @@ class LocalStore:
         self.ivf.add_from(self.index, self.index.rows)
 
     def _maybe_screen(self):
-        """Large bf16/f16 stores (d 768 / 1024) answer batched searches (> 64 questions) with the
-        exact two-pass scan: an int8 copy of the rows (dim bytes per row, kept current
-        by every append / tombstone inside librfx) screened on the i8 matrix cores, the survivors
-        re-scored exactly.  RFX_SCREEN=auto (default: from RFX_SCREEN_MIN_ROWS rows, 262,144) | 1
-        (always) | 0 (never).  Results are the exact scan's either way."""
+        """Large stores (d 768 / 1024) answer with the exact two-pass scan: an int8
+        copy of the rows (dim bytes per row, kept current by every append / tombstone inside librfx)
+        screened on the i8 matrix cores (kernel 10: bf16/f16 batches of > 64 questions) or with
+        v_dot4 (kernel 11: up to 8 questions, any dtype), the survivors re-scored exactly.
+        RFX_SCREEN=auto (default: from RFX_SCREEN_MIN_ROWS rows, 65,536) | 1 (always) | 0 (never).
+        Results are the exact scan's either way."""
         mode = os.environ.get("RFX_SCREEN", "auto")
         if mode == "0" or self._screen_on or not hasattr(self.index, "enable_screen"):
             return
-        if self.dtype not in ("bf16", "f16") or self.dim not in (768, 1024) or self.index.rows == 0:
+        if self.dtype not in ("bf16", "f16", "f32") or self.dim not in (768, 1024) or self.index.rows == 0:
             return
-        if mode != "1" and self.index.rows < int(os.environ.get("RFX_SCREEN_MIN_ROWS", "262144")):
+        if mode != "1" and self.index.rows < int(os.environ.get("RFX_SCREEN_MIN_ROWS", "65536")):
             return
         self.index.enable_screen(1)
         self._screen_on = True

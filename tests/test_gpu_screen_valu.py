@@ -1,0 +1,133 @@
+"""GPU: kernel 11 (k_screen_valu.hip) — the exact two-pass scan of a few questions
+(nq <= 8, 5 <= k <= 16) in one launch over the index's int8 copy, with the gated exact one-launch
+search behind it.  Config 2 (100k x 768 f32, nq 1, k 10) is this path.
+
+Bars (as tests/test_gpu_screen.py): the f32 int8 copy is BIT-EXACT with oracle/screen.py; every
+search returns oracle/search.py's brute-force top-k under check_topk (rows identical outside the
+2e-6 tie band, no duplicates, scores within 1e-5 of the f64 score); the forced fallback (screen
+mode 2) and the exact scan (screen off) return the same rows."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import screen as oscreen
+from oracle import search as osearch
+from oracle import synth as osynth
+
+pytestmark = pytest.mark.gpu
+
+TOL, TIE = 1e-5, 2e-6
+
+
+@pytest.fixture(scope="module")
+def rindex():
+    assert torch.cuda.is_available(), "GPU tests need a GPU"
+    import rfx.index as ri
+    return ri
+
+
+def _widen(stored, dtype):
+    return osynth.to_f64(stored, dtype).astype(np.float32)
+
+
+def _make(rindex, n, d, dtype, seed=31, screen=1):
+    ix = rindex.DeviceIndex(d, dtype)
+    ix.add_synthetic(seed, n)
+    if screen:
+        ix.enable_screen(screen)
+    return ix, _widen(osynth.synth_rows(seed, 0, n, d, dtype), dtype)
+
+
+def _queries(rindex, nq, d, dtype, seed=32):
+    return rindex.synth_rows(seed, 0, nq, d, dtype), _widen(osynth.synth_rows(seed, 0, nq, d, dtype), dtype)
+
+
+def _check(ix, rows32, q, q32, k, row_mask=None, allowed=None):
+    s, r = ix.search(q, k, row_mask=row_mask)
+    torch.cuda.synchronize()
+    s, r = s.cpu().numpy(), r.cpu().numpy()
+    rows64 = rows32.astype(np.float64)
+    if allowed is not None:
+        rows64 = rows64.copy()
+        rows64[~allowed] = np.nan
+    q64 = q32.astype(np.float64)
+    ref_s, ref_r = osearch.topk(q64, rows64, k)
+    probs = osearch.check_topk(s, r, ref_s, ref_r, lambda qi, rr: rows64[rr] @ q64[qi], tol=TOL, tie_band=TIE)
+    assert not probs, probs[:5]
+    return s, r
+
+
+def test_f32_int8_copy_bit_exact(rindex):
+    n = 4000 + 9
+    ix, rows32 = _make(rindex, n, 768, "f32")
+    ix.tombstone([5, 100, 4008])
+    rows32[[5, 100, 4008]] = np.nan
+    codes, scales, live, stats = ix.screen_read(0, (n + 31) // 32)
+    rc, rs, rl, rst = oscreen.quantize_tiles(rows32)
+    assert codes.tobytes() == rc.tobytes() and scales.tobytes() == rs.tobytes() and live.tobytes() == rl.tobytes()
+    assert np.allclose(stats[:2], rst[:2], rtol=2e-7, atol=0) and stats[2] == rst[2]
+
+
+@pytest.mark.parametrize("dtype,d", [("f32", 768), ("bf16", 768), ("f16", 768), ("f32", 1024), ("bf16", 1024)])
+@pytest.mark.parametrize("nq,k", [(1, 10), (3, 5), (8, 16)])
+def test_kernel11_matches_oracle(rindex, dtype, d, nq, k):
+    ix, rows32 = _make(rindex, 30000, d, dtype)
+    assert ix.search_plan(nq, k) == 11
+    q, q32 = _queries(rindex, nq, d, dtype)
+    _check(ix, rows32, q, q32, k)
+
+
+def test_config2_shape(rindex):
+    """BASELINE configs[1]: 100k x 768 f32, one query, k 10 — 20 different lone questions."""
+    ix, rows32 = _make(rindex, 100_000, 768, "f32")
+    q, q32 = _queries(rindex, 20, 768, "f32", seed=1)
+    for i in range(20):
+        _check(ix, rows32, q[i:i + 1].contiguous(), q32[i:i + 1], 10)
+
+
+def test_kernel11_fallback_and_exact_agree(rindex):
+    ix, rows32 = _make(rindex, 40000, 768, "f32")
+    q, q32 = _queries(rindex, 4, 768, "f32")
+    s1, r1 = _check(ix, rows32, q, q32, 10)
+    ix.enable_screen(2)  # the screen declines every batch: the gated exact search answers
+    s2, r2 = _check(ix, rows32, q, q32, 10)
+    ix.enable_screen(0)
+    assert ix.search_plan(4, 10) == 0
+    s3, r3 = _check(ix, rows32, q, q32, 10)
+    assert np.array_equal(r1, r3) and np.array_equal(r2, r3)
+    # the state left behind by a fallback does not leak into the next screened search
+    ix.enable_screen(1)
+    s4, r4 = _check(ix, rows32, q, q32, 10)
+    assert np.array_equal(r4, r3)
+
+
+def test_kernel11_duplicates_tombstones_masks(rindex):
+    ix, rows32 = _make(rindex, 20000, 768, "bf16", screen=0)
+    q, q32 = _queries(rindex, 2, 768, "bf16")
+    top = int(osearch.topk(q32[:1].astype(np.float64), rows32.astype(np.float64), 1)[1][0, 0])
+    # 40 copies of query 0's winner: more than a wave list holds -> dropped rows at the bound -> fallback
+    first = ix.add(ix.read(top, 1).repeat(40, 1))
+    rows32 = np.concatenate([rows32, np.repeat(rows32[top:top + 1], 40, axis=0)])
+    ix.enable_screen(1)
+    s, r = _check(ix, rows32, q, q32, 16)
+    assert r[0, 0] == top and list(r[0, 1:16]) == list(range(first, first + 15))
+    dead = [top, first + 3, 777]
+    ix.tombstone(dead)
+    rows32[dead] = np.nan
+    _check(ix, rows32, q, q32, 10)
+    rng = np.random.default_rng(5)
+    allowed = rng.random(rows32.shape[0]) < 0.25
+    words = np.zeros((rows32.shape[0] + 31) // 32, dtype=np.uint32)
+    for i in np.nonzero(allowed)[0]:
+        words[i >> 5] |= np.uint32(1 << (i & 31))
+    m = torch.from_numpy(words.view(np.int32)).cuda()
+    _check(ix, rows32, q, q32, 10, row_mask=m, allowed=allowed & ~np.isnan(rows32[:, 0]))
+
+
+def test_kernel11_small_stores(rindex):
+    for n in (3, 17, 100, 700):  # fewer rows than k, sub-tile, a few waves
+        ix, rows32 = _make(rindex, n, 768, "f32", seed=40 + n)
+        q, q32 = _queries(rindex, 1, 768, "f32")
+        s, r = _check(ix, rows32, q, q32, 10)
+        if n < 10:
+            assert (r[0, n:] == -1).all()
