@@ -174,14 +174,14 @@ def main():
     r0, r1 = rdist.shard_range(a.rows, rank, world)
     n_local = r1 - r0
     esz = {"bf16": 2, "f16": 2, "f32": 4}[a.dtype]
-    copies = a.copies or min(8, max(1, -(-(768 << 20) // max(n_local * row_bytes, 1)) + 1))
-    if copies > 1 and n_local * row_bytes > (1 << 30):
-        copies = 1  # far beyond the Infinity Cache already
     # the exact two-pass scan: kernel 10 for batches (bf16/f16, nq > 64, k <= 10), kernel 11 for a few
     # questions (any dtype, nq <= 8, 5 <= k <= 16; config 2)
     screen = a.scan == "auto" and a.dim in (768, 1024) and (
         (a.dtype in ("bf16", "f16") and a.nq > 64 and a.k <= 10) or (a.nq <= 8 and 5 <= a.k <= 16))
     row_bytes = a.dim if screen else a.dim * esz  # what a scan streams per row
+    copies = a.copies or min(8, max(1, -(-(768 << 20) // max(n_local * row_bytes, 1)) + 1))
+    if copies > 1 and n_local * row_bytes > (1 << 30):
+        copies = 1  # far beyond the Infinity Cache already
     ixs, build_s = [], 0.0
     for _ in range(copies):
         c = DeviceIndex(a.dim, a.dtype, local, capacity=n_local)

@@ -1,7 +1,7 @@
 // k10_dbg.hip — DEBUG BUILD ONLY (librfx_dbg.so, `make dbg`): ablations and ring depths of the
 // two-pass scan's int8 screen (k_scan_screen.h MODE bits: 1 no top-k fold, 2 no launder, 4 prefetch
-// distance 1, 8 no corpus stream, 64 store-wide integer fast-path bound, 128 epilogue in place, 256 min-of-KL slot bound),
-// via rfx_dbg_screen_variant; variant = 100 * RING + MODE (RING in {4, 6, 8, 10, 12}).
+// distance 1, 8 no corpus stream, 64 store-wide integer fast-path bound, 128 epilogue in place, 256 min-of-KL slot bound, 512 slow path never taken),
+// via rfx_dbg_screen_variant; variant = 1000 * RING + MODE (RING in {4, 6, 8, 10, 12}).
 #include "k_scan_screen.h"
 
 namespace rfx {
@@ -14,7 +14,7 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
   const int ntiles = (nrows + k10::kTM - 1) / k10::kTM;
   dim3 grid(p.blocks, p.q_blocks);
 #define RFX_K10V(R, M)                                                                                        \
-  case 100 * R + M:                                                                                          \
+  case 1000 * R + M:                                                                                          \
     hipLaunchKernelGGL((k10::scan_screen_kernel<10, 768, false, R, M>), grid, dim3(512), 0, st, X, tm, sts, Qc, \
                        qe2, nq, ntiles, tau, cs, cr, dr, p.n_lists, nullptr);                                \
     break;
@@ -39,6 +39,7 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
     RFX_K10V(8, 129)
     RFX_K10V(8, 256)
     RFX_K10V(8, 288)
+    RFX_K10V(8, 512)
     default:
       return -1;
   }

@@ -166,7 +166,8 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
 // LDS only; wrong scores, timing only), 32 = count slow-path entries (threshold slot 15 of each
 // wave's first query), 64 = the fast path on the store-wide integer bound (max tile scale) instead
 // of the tile's own scale, 128 = the epilogue in place at each tile's end (no alternating accumulators),
-// 256 = kernel 6's slot-table bound (min over KL slots) instead of the KL-th largest of 16.
+// 256 = kernel 6's slot-table bound (min over KL slots) instead of the KL-th largest of 16, 512 = the
+// slow path compiled in but never taken (wrong results; separates its cost from the code's presence).
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
@@ -351,6 +352,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
       const float st_t = *(const float*)(lds + kMetaOff + (it % kMR) * 1024 + lane * 16);
       hit = (float)(odd ? m1 : m0) * st_t >= tf_own || (float)(odd ? m0 : m1) * st_t >= tf_oth;
     }
+    if constexpr ((MODE & 512) != 0) hit = hit && nq < 0;  // debug: the slow path compiled in, never taken
     if constexpr ((MODE & 1) == 0) {
       if (__builtin_amdgcn_ballot_w64(hit)) {
         if constexpr ((MODE & 32) != 0)  // debug: count slow-path entries per wave (unused threshold slot 15)
