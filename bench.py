@@ -287,6 +287,8 @@ def main():
             got_s, got_r = out
             full = DeviceIndex(a.dim, a.dtype, local, capacity=a.rows)
             full.add_synthetic(a.seed, a.rows)
+            if screen:  # the same scan as the shards (its scores are the exact re-score's)
+                full.enable_screen(1)
             ref_s, ref_r = full.search(q, a.k)
             if not (torch.equal(got_r, ref_r) and torch.equal(got_s, ref_s)):
                 raise SystemExit("--check: sharded result differs from the whole-index search")
