@@ -11,10 +11,12 @@
 // A >= LB - e2.  Here:
 //   * each wave keeps the K best A of its rows per query (WaveList) and dmax, the best A it had to
 //     drop (rejected or evicted); the block merges its 4 wave lists (dropping into dmax too);
-//   * the block publishes its list's K-th A to the query's bound (agent atomic max): the max over
-//     blocks, LB, is a lower bound of a_K (a block list holds K distinct live rows);
+//   * each wave publishes its list after its first 64 rows, and the block its merged list at the
+//     end, to the query's 16 bound slots (row r to slot r % 16, agent atomic max): a slot holds the
+//     A of one live row and different slots hold different rows, so the k-th largest slot, LB, is a
+//     lower bound of a_k — and close to it once every wave's first rows are in;
 //   * the block re-scores exactly (f64 sum of exact products, rounded to f32) every list entry with
-//     A >= max(bound read, own K-th) - e2 <= LB - e2, so the entries it skips cannot be in the top-k;
+//     A >= max(k-th slot read, own K-th) - e2 <= LB - e2, so the entries it skips cannot be in the top-k;
 //   * the last block merges the exact scores.  When some dmax reaches LB - e2 a dropped row might
 //     have belonged to the top-k: it sets the gate and the exact search rewrites the answer.
 // Algorithmic bytes: N·d codes + ⌈N/32⌉·16 tile records + the re-scored rows (a few per query).
@@ -45,6 +47,32 @@ __device__ __forceinline__ float unord_f32(uint32_t o) {
   return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
 
+// the k-th largest of a query's 16 bound slots (orderable A; 0 = empty), k <= 16: bitonic sort
+__device__ __forceinline__ uint32_t slots_kth(const uint32_t* sl, int k, bool agent) {
+  uint32_t v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    v[i] = agent ? __hip_atomic_load(sl + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : sl[i];
+#pragma unroll
+  for (int kk = 2; kk <= 16; kk <<= 1)
+#pragma unroll
+    for (int jj = kk >> 1; jj > 0; jj >>= 1)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int l = i ^ jj;
+        if (l > i) {
+          const uint32_t a = v[i], b = v[l];
+          const bool desc = (i & kk) == 0;
+          v[i] = desc ? max(a, b) : min(a, b);
+          v[l] = desc ? min(a, b) : max(a, b);
+        }
+      }
+  uint32_t r = 0u;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) r = i == k - 1 ? v[i] : r;
+  return r;
+}
+
 // D / 16 bytes of int8 codes per lane of a 16-lane row group: chunk c = j + 16 i (16 B each)
 template <int D>
 struct Codes {
@@ -63,12 +91,12 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   constexpr int C = D / 256;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
   const int n_lists = gridDim.x;
-  // state (per index and stream, zero on entry and left zero): [0] arrival counter, [8..16) the
-  // queries' bounds (orderable A), [16..24) their dmax, [24] the fallback gate (written, not reset)
+  // state (per index and stream, zero on entry and left zero): [0] arrival counter, [16..24) the
+  // queries' dmax, [24] the fallback gate (written, not reset), [32 + 16 q ..) query q's bound slots
   uint32_t* const ctr = state;
-  uint32_t* const tauA = state + 8;
   uint32_t* const dmx = state + 16;
   uint32_t* const gate = state + 24;
+  uint32_t* const slots = state + 32;
 
   // ---- 1. query codes and e2 (every block, identically): wave w quantises queries w, w + 4 ------
   __shared__ __attribute__((aligned(16))) int8_t qc_lds[NQT][D];
@@ -215,6 +243,11 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       for (int qi = 0; qi < NQT; ++qi) {
         offer(qi, crow < we ? cand[qi] : __builtin_nanf(""), crow);
         cand[qi] = __builtin_nanf("");
+        // the first chunk's list goes to the bound slots at once: the blocks run in step, so a bound
+        // published only at the end would reach no block in time to prune its re-scoring
+        if (t < 16 && qi < nq && lane < kK && L[qi].lr != kEmptyRow)
+          __hip_atomic_fetch_max(slots + 16 * qi + (L[qi].lr & 15), ord_f32(L[qi].ls), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
@@ -223,11 +256,11 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   __shared__ float ms[4][NQT][kK];
   __shared__ int mr[4][NQT][kK];
   __shared__ float wdm[4][NQT];
-  uint32_t seen[(NQT + 3) / 4];
+  uint32_t seen[(NQT + 3) / 4];  // the k-th slot as it stands now (any value read is a valid bound)
 #pragma unroll
   for (int u = 0; u < (NQT + 3) / 4; ++u) {
     const int qi = w + 4 * u;
-    seen[u] = qi < nq ? __hip_atomic_load(tauA + qi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+    seen[u] = qi < nq ? slots_kth(slots + 16 * qi, k_out, true) : 0u;
   }
 #pragma unroll
   for (int qi = 0; qi < NQT; ++qi) {
@@ -264,9 +297,12 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     for (int off = 32; off; off >>= 1) d = fmaxf(d, __shfl_xor(d, off));
     const float kth = readlane_f(M.ls, kK - 1);
     const bool full = readlane_i(M.lr, kK - 1) != kEmptyRow;
-    if (lane == 0 && qi < nq) {
-      if (full) __hip_atomic_fetch_max(tauA + qi, ord_f32(kth), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (d > -__builtin_inff()) __hip_atomic_fetch_max(dmx + qi, ord_f32(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (qi < nq) {
+      if (lane < kK && M.lr != kEmptyRow)
+        __hip_atomic_fetch_max(slots + 16 * qi + (M.lr & 15), ord_f32(M.ls), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0 && d > -__builtin_inff())
+        __hip_atomic_fetch_max(dmx + qi, ord_f32(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const uint32_t sn = seen[(qi - w) / 4];
     float b = sn ? unord_f32(sn) : -__builtin_inff();
@@ -279,29 +315,38 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   }
   __syncthreads();
 
-  // ---- 4. exact re-score of the block's entries at or above its cut (wave per entry) -------------
-  // lane covers elements lane + 64 e of the row; products of stored values are exact in f64
-  constexpr int PL = D / 64;
-  for (int e = w; e < NQT * kK; e += 4) {
-    const int qi = e / kK, i = e - qi * kK;
-    const int r = bR[qi][i];
-    const bool go = qi < nq && r != kEmptyRow && bA[qi][i] >= bCut[qi];
-    float sc = -__builtin_inff();
-    if (go) {  // wave-uniform
+  // ---- 4. exact re-score of the block's entries at or above its cut: 16 lanes per entry, 16 entries
+  // at a time, every row's loads in flight together (one memory latency per round) ---------------
+  {
+    constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
+    constexpr int EPV = 16 / ESZ;         // elements per 16-B load
+    constexpr int VPL = D * ESZ / 256;    // 16-B loads per lane (a 16-lane group covers the row)
+    const int grp = tid >> 4, gl = tid & 15;
+    for (int e0 = 0; e0 < NQT * kK; e0 += 16) {
+      const int e = e0 + grp, qi = e / kK, i = e - qi * kK;
+      const int r = bR[qi][i];
+      const bool go = qi < nq && r != kEmptyRow && bA[qi][i] >= bCut[qi];
       double acc = 0.0;
+      if (go) {
+        uint4 xv[VPL], yv[VPL];
 #pragma unroll
-      for (int u = 0; u < PL; ++u) {
-        const int64_t idx = (int64_t)r * D + lane + 64 * u;
-        acc += (double)qelem<DT>(X, idx) * (double)qelem<DT>(Q, (int64_t)qi * D + lane + 64 * u);
+        for (int u = 0; u < VPL; ++u) {
+          xv[u] = *(const uint4*)((const uint8_t*)X + (int64_t)r * D * ESZ + (int64_t)(gl + 16 * u) * 16);
+          yv[u] = *(const uint4*)((const uint8_t*)Q + (int64_t)qi * D * ESZ + (int64_t)(gl + 16 * u) * 16);
+        }
+#pragma unroll
+        for (int u = 0; u < VPL; ++u)
+#pragma unroll
+          for (int ee = 0; ee < EPV; ++ee) acc += (double)elem<DT>(xv[u], ee) * (double)elem<DT>(yv[u], ee);
       }
 #pragma unroll
-      for (int off = 32; off; off >>= 1) acc += __shfl_xor(acc, off);
-      sc = (float)acc;
-    }
-    if (lane == 0 && qi < nq) {
-      const int64_t o = ((int64_t)qi * n_lists + blockIdx.x) * kK + i;
-      __hip_atomic_store((uint32_t*)cand_s + o, __float_as_uint(sc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(cand_r + o, go ? r : kEmptyRow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int off = 8; off; off >>= 1) acc += __shfl_xor(acc, off);  // within the 16-lane group
+      if (gl == 0 && qi < nq) {
+        const int64_t o = ((int64_t)qi * n_lists + blockIdx.x) * kK + i;
+        __hip_atomic_store((uint32_t*)cand_s + o, __float_as_uint(go ? (float)acc : -__builtin_inff()),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(cand_r + o, go ? r : kEmptyRow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
   }
 
@@ -319,9 +364,9 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   if (tid == 0) fail = force;
   __syncthreads();
   if (tid < nq) {
-    const uint32_t lb = __hip_atomic_load(tauA + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t lb = slots_kth(slots + 16 * tid, k_out, true);
     const uint32_t d = __hip_atomic_load(dmx + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // no bound (no block list full) with drops, or a drop at or above LB - e2: not proven
+    // no bound (fewer than k slots filled) with drops, or a drop at or above LB - e2: not proven
     if (d && (!lb || unord_f32(d) >= unord_f32(lb) - e2_lds[tid])) atomicOr(&fail, 1);
   }
   __syncthreads();
@@ -344,10 +389,8 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       __syncthreads();
     }
   }
-  if (tid < 8) {
-    tauA[tid] = 0u;
-    dmx[tid] = 0u;
-  }
+  if (tid < 8) dmx[tid] = 0u;
+  if (tid < 8 * 16) slots[tid] = 0u;
   if (tid == 0) {
     *gate = fail ? 1u : 0u;  // read by the gated exact search that follows on the stream
     *ctr = 0u;

@@ -37,9 +37,10 @@ int launch_scan_valu(const ValuPlan& p, const void* X, int nrows, int D, int dty
 // p.q_slices arrival counters, ALL ZERO on entry — the kernel leaves them zero again, so a state
 // buffer zeroed once serves every later search on one stream (rfx_api.hip keeps one per stream).
 constexpr int kValuFusedMaxNq = 1024;
-// + 32 words for the lone-question two-pass scan (kernel 11): counter, bounds, drops, fallback gate
+// + 160 words for the lone-question two-pass scan (kernel 11): counter, drops, fallback gate, and
+// 16 bound slots for each of up to 8 queries
 constexpr int kScreenValuState = kValuFusedMaxNq + 1024;
-constexpr int kValuFusedStateWords = kScreenValuState + 32;
+constexpr int kValuFusedStateWords = kScreenValuState + 160;
 // gate (optional): the launch runs only when *gate != 0 (the two-pass scan's fallback)
 int launch_search_valu_fused(const ValuPlan& p, const void* X, int nrows, int D, int dtype, const void* Q, int nq,
                              float* cs, int* cr, uint32_t* state, int k, float* out_s, int64_t* out_r,
