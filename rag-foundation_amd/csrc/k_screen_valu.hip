@@ -6,26 +6,27 @@
 //
 // Path: the retrieval half of GeminiRag.ask_stream (backend/app/services/gemini_rag.py:517-551).
 // The int8 copy and the exactness argument are kernel 10's (k_scan_screen.h): per
-// 32-row tile scale s_t, per query s_y and e2 = 2 E_q / s_y (rounded up), screen score A = s_t D.
-// With LB <= a_K (the K-th best A over live rows, K >= k) every row of the exact top-k has
-// A >= LB - e2.  Here:
-//   * each wave keeps the K best A of its rows per query (WaveList) and dmax, the best A it had to
-//     drop (rejected or evicted); the block merges its 4 wave lists (dropping into dmax too);
-//   * each wave publishes its list after its first 64 rows, and the block its merged list at the
-//     end, to the query's 16 bound slots (row r to slot r % 16, agent atomic max): a slot holds the
-//     A of one live row and different slots hold different rows, so the k-th largest slot, LB, is a
-//     lower bound of a_k — and close to it once every wave's first rows are in;
-//   * the block re-scores exactly (f64 sum of exact products, rounded to f32) every list entry with
-//     A >= max(k-th slot read, own K-th) - e2 <= LB - e2, so the entries it skips cannot be in the top-k;
-//   * the last block merges the exact scores.  When some dmax reaches LB - e2 a dropped row might
-//     have belonged to the top-k: it sets the gate and the exact search rewrites the answer.
+// 32-row tile scale s_t, per query s_y and e2 = 2 E_q / s_y (rounded up), screen score A = s_t D;
+// every row of the exact top-k has A >= a_k - e2 (a_k: the k-th best A over live rows).  Here:
+//   * each wave keeps the 16 best A of its rows per query (WaveList) and the best A it had to drop
+//     (rejected or evicted); the block merges its four wave lists and writes a record per query:
+//     its 15 best (A, row) and, in entry 15, its drop bound (everything it did not keep is <= it);
+//   * the last block to finish (agent-scope arrival counter) takes a_k' = the k-th best A over all
+//     records (a lower bound of a_k: the records hold distinct live rows).  If some drop bound
+//     reaches a_k' - e2 a dropped row might belong to the top-k: it sets the gate and the exact
+//     one-launch search that follows rewrites the answer.  Otherwise every row with
+//     A >= a_k' - e2 (the top-k among them, as a_k' <= a_k) is in a record: it re-scores those survivors exactly (f64 sum of the
+//     exact products, rounded to f32, 16 lanes per row) and ranks them (score desc, row asc).
+// No atomics on shared addresses besides the arrival counter: the bound travels in the records.
 // Algorithmic bytes: N·d codes + ⌈N/32⌉·16 tile records + the re-scored rows (a few per query).
 #include "k_scan_valu.h"
 
 namespace rfx {
 namespace {
 
-constexpr int kK = 16;  // A-list length (k <= 16)
+constexpr int kK = 16;           // A-list length (k <= 16)
+constexpr int kDropRow = -2;     // record entry 15: the block's drop bound, not a row
+constexpr int kSurvCap = 1024;   // survivors re-scored by the last block; more -> the exact fallback
 
 template <int DT>
 __device__ __forceinline__ float qelem(const void* Q, int64_t i) {
@@ -47,37 +48,12 @@ __device__ __forceinline__ float unord_f32(uint32_t o) {
   return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
 
-// the k-th largest of a query's 16 bound slots (orderable A; 0 = empty), k <= 16: bitonic sort
-__device__ __forceinline__ uint32_t slots_kth(const uint32_t* sl, int k, bool agent) {
-  uint32_t v[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i)
-    v[i] = agent ? __hip_atomic_load(sl + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : sl[i];
-#pragma unroll
-  for (int kk = 2; kk <= 16; kk <<= 1)
-#pragma unroll
-    for (int jj = kk >> 1; jj > 0; jj >>= 1)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int l = i ^ jj;
-        if (l > i) {
-          const uint32_t a = v[i], b = v[l];
-          const bool desc = (i & kk) == 0;
-          v[i] = desc ? max(a, b) : min(a, b);
-          v[l] = desc ? min(a, b) : max(a, b);
-        }
-      }
-  uint32_t r = 0u;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) r = i == k - 1 ? v[i] : r;
-  return r;
-}
-
 // D / 16 bytes of int8 codes per lane of a 16-lane row group: chunk c = j + 16 i (16 B each)
 template <int D>
 struct Codes {
   static constexpr int C = D / 256;  // 16-B chunks per lane (3 at d 768, 4 at d 1024)
   uint4 v[C];
+  uint4 md;  // the row's tile record {scale, live word}, loaded with the codes (prefetched alike)
 };
 
 template <int DT, int D, int NQT>
@@ -91,12 +67,10 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   constexpr int C = D / 256;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
   const int n_lists = gridDim.x;
-  // state (per index and stream, zero on entry and left zero): [0] arrival counter, [16..24) the
-  // queries' dmax, [24] the fallback gate (written, not reset), [32 + 16 q ..) query q's bound slots
+  // state (per index and stream): [0] the arrival counter (zero on entry, left zero), [24] the
+  // fallback gate (written by the last block, read by the gated exact search)
   uint32_t* const ctr = state;
-  uint32_t* const dmx = state + 16;
   uint32_t* const gate = state + 24;
-  uint32_t* const slots = state + 32;
 
   // ---- 1. query codes and e2 (every block, identically): wave w quantises queries w, w + 4 ------
   __shared__ __attribute__((aligned(16))) int8_t qc_lds[NQT][D];
@@ -165,13 +139,15 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   }
   auto load_row = [&](int t, Codes<D>& v) {
     const int row = wb + 64 * (t >> 4) + 4 * (t & 15) + g;
-    const int8_t* rp = X8 + (int64_t)(row < we ? row : wb) * D;
+    const int rr = row < we ? row : wb;
+    const int8_t* rp = X8 + (int64_t)rr * D;
 #pragma unroll
     for (int i = 0; i < C; ++i) v.v[i] = *(const uint4*)(rp + 16 * (j + 16 * i));
+    v.md = tmeta[rr >> 5];  // cache hits after the first row of a tile
   };
   auto score_row = [&](int t, const Codes<D>& v) {
     const int row = wb + 64 * (t >> 4) + 4 * (t & 15) + g;
-    const uint4 md = tmeta[(row < we ? row : wb) >> 5];  // the tile's {scale, live word}: cache hits
+    const uint4 md = v.md;
     const float st = __uint_as_float(md.x);
 #pragma unroll
     for (int qi = 0; qi < NQT; ++qi) {
@@ -185,7 +161,9 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       }
       const float dsum = row16_sum((float)acc);  // |partial sums| < 2^24: exact in f32
       const float a = dsum * st;                 // A = s_t D, one rounding (as kernel 10)
-      const bool live = row < we && ((md.y >> (row & 31)) & 1u) && (mask == nullptr || row_allowed(mask, row));
+      // the tile's live bit only: the row mask is read once per chunk at offer time (a load under a
+      // condition here would end in a vmcnt(0) drain of the row stream at every row)
+      const bool live = row < we && ((md.y >> (row & 31)) & 1u);
       if (j == (t & 15)) cand[qi] = live ? a : __builtin_nanf("");
     }
   };
@@ -239,29 +217,19 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     score_row(t + 3, vd);
     if (((t + 4) & 15) == 0 || t + 4 >= T) {  // a 64-row chunk scored: every lane holds one row
       const int crow = wb + 64 * (t >> 4) + j * 4 + g;
+      const bool ok = crow < we && (mask == nullptr || row_allowed(mask, crow));
 #pragma unroll
       for (int qi = 0; qi < NQT; ++qi) {
-        offer(qi, crow < we ? cand[qi] : __builtin_nanf(""), crow);
+        offer(qi, ok ? cand[qi] : __builtin_nanf(""), crow);
         cand[qi] = __builtin_nanf("");
-        // the first chunk's list goes to the bound slots at once: the blocks run in step, so a bound
-        // published only at the end would reach no block in time to prune its re-scoring
-        if (t < 16 && qi < nq && lane < kK && L[qi].lr != kEmptyRow)
-          __hip_atomic_fetch_max(slots + 16 * qi + (L[qi].lr & 15), ord_f32(L[qi].ls), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
 
-  // ---- 3. block list per query, its K-th A published, bound read --------------------------------
+  // ---- 3. block record per query: the 15 best A of the block (rows), and its drop bound ----------
   __shared__ float ms[4][NQT][kK];
   __shared__ int mr[4][NQT][kK];
   __shared__ float wdm[4][NQT];
-  uint32_t seen[(NQT + 3) / 4];  // the k-th slot as it stands now (any value read is a valid bound)
-#pragma unroll
-  for (int u = 0; u < (NQT + 3) / 4; ++u) {
-    const int qi = w + 4 * u;
-    seen[u] = qi < nq ? slots_kth(slots + 16 * qi, k_out, true) : 0u;
-  }
 #pragma unroll
   for (int qi = 0; qi < NQT; ++qi) {
     if (lane < kK) {
@@ -274,10 +242,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     if (lane == 0) wdm[w][qi] = d;
   }
   __syncthreads();
-  __shared__ float bA[NQT][kK];
-  __shared__ int bR[NQT][kK];
-  __shared__ float bCut[NQT];
-  for (int qi = w; qi < NQT; qi += 4) {
+  for (int qi = w; qi < nq; qi += 4) {
     WaveList<kK> M;
     M.init();
 #pragma unroll
@@ -285,72 +250,28 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       const bool v = lane < kK && mr[src][qi][lane] != kEmptyRow;
       M.offer(v ? ms[src][qi][lane] : -__builtin_inff(), v ? mr[src][qi][lane] : kEmptyRow, v);
     }
-    // entries of the wave lists the block list does not hold: strictly worse than its K-th entry
+    // dropped: the waves' drops, wave-list entries the block list does not hold (strictly worse
+    // than its 16th), and the 16th itself (entry 15 of the record carries the drop bound instead)
     float d = fmaxf(fmaxf(wdm[0][qi], wdm[1][qi]), fmaxf(wdm[2][qi], wdm[3][qi]));
 #pragma unroll
     for (int src = 0; src < 4; ++src) {
       const bool v = lane < kK && mr[src][qi][lane] != kEmptyRow;
-      const float s = v ? ms[src][qi][lane] : -__builtin_inff();
-      if (v && better(M.ts, M.tr, s, mr[src][qi][lane])) d = fmaxf(d, s);
+      const float sv = v ? ms[src][qi][lane] : -__builtin_inff();
+      if (v && better(M.ts, M.tr, sv, mr[src][qi][lane])) d = fmaxf(d, sv);
     }
+    if (lane == kK - 1 && M.lr != kEmptyRow) d = fmaxf(d, M.ls);
 #pragma unroll
     for (int off = 32; off; off >>= 1) d = fmaxf(d, __shfl_xor(d, off));
-    const float kth = readlane_f(M.ls, kK - 1);
-    const bool full = readlane_i(M.lr, kK - 1) != kEmptyRow;
-    if (qi < nq) {
-      if (lane < kK && M.lr != kEmptyRow)
-        __hip_atomic_fetch_max(slots + 16 * qi + (M.lr & 15), ord_f32(M.ls), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-      if (lane == 0 && d > -__builtin_inff())
-        __hip_atomic_fetch_max(dmx + qi, ord_f32(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const uint32_t sn = seen[(qi - w) / 4];
-    float b = sn ? unord_f32(sn) : -__builtin_inff();
-    if (full) b = fmaxf(b, kth);
     if (lane < kK) {
-      bA[qi][lane] = M.ls;
-      bR[qi][lane] = M.lr;
-    }
-    if (lane == 0) bCut[qi] = b > -__builtin_inff() ? b - e2_lds[qi] : -__builtin_inff();
-  }
-  __syncthreads();
-
-  // ---- 4. exact re-score of the block's entries at or above its cut: 16 lanes per entry, 16 entries
-  // at a time, every row's loads in flight together (one memory latency per round) ---------------
-  {
-    constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
-    constexpr int EPV = 16 / ESZ;         // elements per 16-B load
-    constexpr int VPL = D * ESZ / 256;    // 16-B loads per lane (a 16-lane group covers the row)
-    const int grp = tid >> 4, gl = tid & 15;
-    for (int e0 = 0; e0 < NQT * kK; e0 += 16) {
-      const int e = e0 + grp, qi = e / kK, i = e - qi * kK;
-      const int r = bR[qi][i];
-      const bool go = qi < nq && r != kEmptyRow && bA[qi][i] >= bCut[qi];
-      double acc = 0.0;
-      if (go) {
-        uint4 xv[VPL], yv[VPL];
-#pragma unroll
-        for (int u = 0; u < VPL; ++u) {
-          xv[u] = *(const uint4*)((const uint8_t*)X + (int64_t)r * D * ESZ + (int64_t)(gl + 16 * u) * 16);
-          yv[u] = *(const uint4*)((const uint8_t*)Q + (int64_t)qi * D * ESZ + (int64_t)(gl + 16 * u) * 16);
-        }
-#pragma unroll
-        for (int u = 0; u < VPL; ++u)
-#pragma unroll
-          for (int ee = 0; ee < EPV; ++ee) acc += (double)elem<DT>(xv[u], ee) * (double)elem<DT>(yv[u], ee);
-      }
-#pragma unroll
-      for (int off = 8; off; off >>= 1) acc += __shfl_xor(acc, off);  // within the 16-lane group
-      if (gl == 0 && qi < nq) {
-        const int64_t o = ((int64_t)qi * n_lists + blockIdx.x) * kK + i;
-        __hip_atomic_store((uint32_t*)cand_s + o, __float_as_uint(go ? (float)acc : -__builtin_inff()),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(cand_r + o, go ? r : kEmptyRow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+      const int64_t o = ((int64_t)qi * n_lists + blockIdx.x) * kK + lane;
+      const bool rec = lane < kK - 1;
+      __hip_atomic_store((uint32_t*)cand_s + o, __float_as_uint(rec ? M.ls : d), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(cand_r + o, rec ? M.lr : kDropRow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 
-  // ---- 5. the last block: check the drops against LB - e2, merge the exact scores ---------------
+  // ---- 4. the last block: a_k from the records, the drop check, survivors, exact re-score, top-k --
   __shared__ int last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -360,37 +281,121 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   }
   __syncthreads();
   if (!last) return;
-  __shared__ int fail;
+  const int n = n_lists * kK;  // <= kFusedLdsCand (host check)
+  __shared__ float bs[kFusedLdsCand];
+  __shared__ int br[kFusedLdsCand];
+  __shared__ int sv[kSurvCap];    // survivor -> record index
+  __shared__ float sx[kSurvCap];  // its exact score
+  __shared__ float wk[4][kK];
+  __shared__ int wr[4][kK];
+  __shared__ float red[4];
+  __shared__ int n_sv, fail;
+  __shared__ float cut;
   if (tid == 0) fail = force;
-  __syncthreads();
-  if (tid < nq) {
-    const uint32_t lb = slots_kth(slots + 16 * tid, k_out, true);
-    const uint32_t d = __hip_atomic_load(dmx + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // no bound (fewer than k slots filled) with drops, or a drop at or above LB - e2: not proven
-    if (d && (!lb || unord_f32(d) >= unord_f32(lb) - e2_lds[tid])) atomicOr(&fail, 1);
-  }
-  __syncthreads();
-  if (!fail) {
-    const int64_t n = (int64_t)n_lists * kK;
-    __shared__ float bs[kFusedLdsCand];
-    __shared__ int br[kFusedLdsCand];
-    for (int qi = 0; qi < nq; ++qi) {
-      const int64_t qo = (int64_t)qi * n;
-      if (n <= kFusedLdsCand) {
-        for (int i = tid; i < (int)n; i += 256) {
-          bs[i] = __uint_as_float(__hip_atomic_load((const uint32_t*)cand_s + qo + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          br[i] = __hip_atomic_load(cand_r + qo + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int qi = 0; qi < nq; ++qi) {
+    for (int i = tid; i < n; i += 256) {
+      const int64_t o = (int64_t)qi * n + i;
+      bs[i] = __uint_as_float(__hip_atomic_load((const uint32_t*)cand_s + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      br[i] = __hip_atomic_load(cand_r + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (tid == 0) n_sv = 0;
+    __syncthreads();
+    // a_k over the records (k_out-th best A, ties by row) and the largest drop bound
+    WaveList<kK> W;
+    W.init();
+    float dmax = -__builtin_inff();
+    const int per = (n + 3) / 4, lo = w * per, hi = min(n, lo + per);
+    for (int b0 = lo; b0 < hi; b0 += 64) {
+      const int i = b0 + lane;
+      const bool in = i < hi;
+      const int r = in ? br[i] : kEmptyRow;
+      const float a = in ? bs[i] : -__builtin_inff();
+      if (r == kDropRow) dmax = fmaxf(dmax, a);
+      W.offer(a, r, in && r != kEmptyRow && r != kDropRow);
+    }
+#pragma unroll
+    for (int off = 32; off; off >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, off));
+    if (lane < kK) {
+      wk[w][lane] = W.ls;
+      wr[w][lane] = W.lr;
+    }
+    if (lane == 0) red[w] = dmax;
+    __syncthreads();
+    if (w == 0) {
+      WaveList<kK> M;
+      M.init();
+#pragma unroll
+      for (int src = 0; src < 4; ++src) {
+        const bool v = lane < kK && wr[src][lane] != kEmptyRow;
+        M.offer(v ? wk[src][lane] : -__builtin_inff(), v ? wr[src][lane] : kEmptyRow, v);
+      }
+      const bool have = readlane_i(M.lr, k_out - 1) != kEmptyRow;
+      const float ak = readlane_f(M.ls, k_out - 1);
+      const float c = have ? ak - e2_lds[qi] : -__builtin_inff();
+      const float dm_all = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+      if (lane == 0) {
+        cut = c;
+        // a dropped row at or above a_k - e2 could belong to the top-k: not proven
+        if (dm_all > -__builtin_inff() && dm_all >= c) fail = 1;
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += 256) {
+      const int r = br[i];
+      if (r != kEmptyRow && r != kDropRow && bs[i] >= cut) {
+        const int j2 = atomicAdd(&n_sv, 1);
+        if (j2 < kSurvCap) sv[j2] = i;
+      }
+    }
+    __syncthreads();
+    if (n_sv > kSurvCap && tid == 0) fail = 1;
+    __syncthreads();
+    if (!fail) {
+      const int ns = n_sv;
+      // exact re-score: 16 lanes per survivor, 16 survivors per round, every row's loads in flight
+      constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
+      constexpr int EPV = 16 / ESZ;
+      constexpr int VPL = D * ESZ / 256;
+      const int grp = tid >> 4, gl = tid & 15;
+      for (int e0 = 0; e0 < ns; e0 += 16) {
+        const int e = e0 + grp;
+        double acc = 0.0;
+        if (e < ns) {
+          const int r = br[sv[e]];
+          uint4 xv[VPL], yv[VPL];
+#pragma unroll
+          for (int u = 0; u < VPL; ++u) {
+            xv[u] = *(const uint4*)((const uint8_t*)X + (int64_t)r * D * ESZ + (int64_t)(gl + 16 * u) * 16);
+            yv[u] = *(const uint4*)((const uint8_t*)Q + (int64_t)qi * D * ESZ + (int64_t)(gl + 16 * u) * 16);
+          }
+#pragma unroll
+          for (int u = 0; u < VPL; ++u)
+#pragma unroll
+            for (int ee = 0; ee < EPV; ++ee) acc += (double)elem<DT>(xv[u], ee) * (double)elem<DT>(yv[u], ee);
         }
-        __syncthreads();
-        merge_one<kK, false, 4, false>(LdsSrc{bs, br, n}, qi, kK, k_out, 0, out_s, out_r, nullptr);
-      } else {
-        merge_one<kK, false, 4, false>(AgentSrc{cand_s, cand_r, n}, qi, kK, k_out, 0, out_s, out_r, nullptr);
+#pragma unroll
+        for (int off = 8; off; off >>= 1) acc += __shfl_xor(acc, off);  // within the 16-lane group
+        if (gl == 0 && e < ns) sx[e] = (float)acc;
       }
       __syncthreads();
+      // top-k of the survivors by (exact score desc, row asc): each survivor counts those ahead of it
+      for (int e = tid; e < ns; e += 256) {
+        const float se = sx[e];
+        const int re = br[sv[e]];
+        int rank = 0;
+        for (int f = 0; f < ns; ++f) rank += better(sx[f], br[sv[f]], se, re);
+        if (rank < k_out) {
+          out_s[(int64_t)qi * k_out + rank] = se;
+          out_r[(int64_t)qi * k_out + rank] = re;
+        }
+      }
+      for (int i = ns + tid; i < k_out; i += 256) {  // fewer survivors than k: padding
+        out_s[(int64_t)qi * k_out + i] = -__builtin_inff();
+        out_r[(int64_t)qi * k_out + i] = -1;
+      }
     }
+    __syncthreads();
   }
-  if (tid < 8) dmx[tid] = 0u;
-  if (tid < 8 * 16) slots[tid] = 0u;
   if (tid == 0) {
     *gate = fail ? 1u : 0u;  // read by the gated exact search that follows on the stream
     *ctr = 0u;
