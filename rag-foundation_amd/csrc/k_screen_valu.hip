@@ -11,8 +11,8 @@
 //   * each wave keeps the 16 best A of its rows per query (WaveList) and the best A it had to drop
 //     (rejected or evicted); the block merges its four wave lists and writes a record per query:
 //     its 15 best (A, row) and, in entry 15, its drop bound (everything it did not keep is <= it);
-//   * the last block to finish (agent-scope arrival counter) takes a_k' = the k-th best A over all
-//     records (a lower bound of a_k: the records hold distinct live rows).  If some drop bound
+//   * the last block to finish (agent-scope arrival counter) takes a_k' = the k-th best A over the
+//     records' best entries (a lower bound of a_k: distinct live rows).  If some drop bound
 //     reaches a_k' - e2 a dropped row might belong to the top-k: it sets the gate and the exact
 //     one-launch search that follows rewrites the answer.  Otherwise every row with
 //     A >= a_k' - e2 (the top-k among them, as a_k' <= a_k) is in a record: it re-scores those survivors exactly (f64 sum of the
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   __shared__ float e2_lds[NQT];
   {
     const double xm = (double)__uint_as_float(stats[0]), em = (double)__uint_as_float(stats[1]);
-    for (int qi = w; qi < NQT; qi += 4) {
+    for (int qi = w; qi < NQT && !(force & 4); qi += 4) {
       constexpr int PL = D / 64;  // elements per lane
       float y[PL];
       float am = 0.f;
@@ -127,7 +127,9 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   const int wave_g = blockIdx.x * 4 + w;
   const int wb = (int)min((int64_t)wave_g * rows_per_wave, (int64_t)nrows);
   const int we = (int)min((int64_t)wb + rows_per_wave, (int64_t)nrows);
-  const int T = we > wb ? (we - wb + 15) / 16 * 4 : 0;
+  // force bits 2/4/8/16/32 (RFX_K11_ABLATE, timing only, wrong results): no row stream / no query
+  // quantiser / no last-block work / no re-score and rank / no LB over the records
+  const int T = (force & 2) ? 0 : we > wb ? (we - wb + 15) / 16 * 4 : 0;
   WaveList<kK> L[NQT];
   float dm[NQT];  // per lane: the best A this wave dropped (rejected at offer time or evicted)
   float cand[NQT];
@@ -200,28 +202,28 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       l.tr = readlane_i(l.lr, kK - 1);
     }
   };
-  Codes<D> va, vb, vc, vd;
+  // NB row buffers: NB - 1 iterations of loads in flight ahead of the one being scored (one wave per
+  // SIMD has nothing else to hide the latency; 3 in flight measured latency-bound at 2.6 TB/s)
+  constexpr int NB = NQT == 1 ? 8 : 4;
+  Codes<D> buf[NB];
   if (T > 0) {
-    load_row(0, va);
-    load_row(1, vb);
-    load_row(2, vc);
-  }
-  for (int t = 0; t < T; t += 4) {
-    load_row(t + 3, vd);
-    score_row(t, va);
-    load_row(t + 4, va);
-    score_row(t + 1, vb);
-    load_row(t + 5, vb);
-    score_row(t + 2, vc);
-    load_row(t + 6, vc);
-    score_row(t + 3, vd);
-    if (((t + 4) & 15) == 0 || t + 4 >= T) {  // a 64-row chunk scored: every lane holds one row
-      const int crow = wb + 64 * (t >> 4) + j * 4 + g;
-      const bool ok = crow < we && (mask == nullptr || row_allowed(mask, crow));
 #pragma unroll
-      for (int qi = 0; qi < NQT; ++qi) {
-        offer(qi, ok ? cand[qi] : __builtin_nanf(""), crow);
-        cand[qi] = __builtin_nanf("");
+    for (int p = 0; p < NB - 1; ++p) load_row(p, buf[p]);
+  }
+  for (int t = 0; t < T; t += NB) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      load_row(t + b + NB - 1, buf[(b + NB - 1) % NB]);  // past T: re-reads of row wb, never offered
+      score_row(t + b, buf[b]);
+      if ((b & 3) == 3 && (((t + b + 1) & 15) == 0 || t + b + 1 >= T)) {
+        // a 64-row chunk scored (or the last, partial one): every lane holds one row
+        const int crow = wb + 64 * ((t + b) >> 4) + j * 4 + g;
+        const bool ok = crow < we && (mask == nullptr || row_allowed(mask, crow));
+#pragma unroll
+        for (int qi = 0; qi < NQT; ++qi) {
+          offer(qi, ok ? cand[qi] : __builtin_nanf(""), crow);
+          cand[qi] = __builtin_nanf("");
+        }
       }
     }
   }
@@ -281,63 +283,99 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   }
   __syncthreads();
   if (!last) return;
+  if (force & 8) {
+    if (tid == 0) {
+      *gate = 0u;
+      *ctr = 0u;
+    }
+    return;
+  }
   const int n = n_lists * kK;  // <= kFusedLdsCand (host check)
   __shared__ float bs[kFusedLdsCand];
   __shared__ int br[kFusedLdsCand];
   __shared__ int sv[kSurvCap];    // survivor -> record index
   __shared__ float sx[kSurvCap];  // its exact score
-  __shared__ float wk[4][kK];
-  __shared__ int wr[4][kK];
   __shared__ float red[4];
   __shared__ int n_sv, fail;
   __shared__ float cut;
-  if (tid == 0) fail = force;
+  __shared__ uint32_t lbk_o;
+  __shared__ __attribute__((aligned(16))) uint32_t hk[1024];
+  if (tid == 0) fail = force & 1;
   for (int qi = 0; qi < nq; ++qi) {
-    for (int i = tid; i < n; i += 256) {
-      const int64_t o = (int64_t)qi * n + i;
-      bs[i] = __uint_as_float(__hip_atomic_load((const uint32_t*)cand_s + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      br[i] = __hip_atomic_load(cand_r + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // bulk copy into LDS with 8 loads per thread in flight (agent-scope loads are not batched by the
+    // compiler: one at a time they cost a memory round trip each — measured 55 us for this select)
+    for (int base = 0; base < n; base += 256 * 8) {
+      uint32_t sv8[8];
+      int rv8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = base + u * 256 + tid;
+        if (i < n) {
+          sv8[u] = __hip_atomic_load((const uint32_t*)cand_s + (int64_t)qi * n + i, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+          rv8[u] = __hip_atomic_load(cand_r + (int64_t)qi * n + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = base + u * 256 + tid;
+        if (i < n) {
+          bs[i] = __uint_as_float(sv8[u]);
+          br[i] = rv8[u];
+        }
+      }
     }
     if (tid == 0) n_sv = 0;
     __syncthreads();
-    // a_k over the records (k_out-th best A, ties by row) and the largest drop bound
-    WaveList<kK> W;
-    W.init();
+    // The largest drop bound, and LB, a lower bound of a_k from each record's best entry (every entry
+    // when the records are few): distinct live rows either way.
     float dmax = -__builtin_inff();
-    const int per = (n + 3) / 4, lo = w * per, hi = min(n, lo + per);
-    for (int b0 = lo; b0 < hi; b0 += 64) {
-      const int i = b0 + lane;
-      const bool in = i < hi;
-      const int r = in ? br[i] : kEmptyRow;
-      const float a = in ? bs[i] : -__builtin_inff();
-      if (r == kDropRow) dmax = fmaxf(dmax, a);
-      W.offer(a, r, in && r != kEmptyRow && r != kDropRow);
-    }
+    for (int i = tid; i < n; i += 256)
+      if (br[i] == kDropRow) dmax = fmaxf(dmax, bs[i]);
 #pragma unroll
     for (int off = 32; off; off >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, off));
-    if (lane < kK) {
-      wk[w][lane] = W.ls;
-      wr[w][lane] = W.lr;
-    }
     if (lane == 0) red[w] = dmax;
+    // heads (or every entry when the records are few) as orderable keys, 0 = none; LB = the best key
+    // with at least k keys at or above it (k distinct live rows reach it): every thread counts for
+    // its key with 16-B broadcast reads of the whole key array, no dependent loads
+    const bool every = n <= 1024;
+    const int m = (force & 32) ? 0 : every ? n : n_lists;  // <= 1024
+    for (int c = tid; c < 1024; c += 256) {
+      uint32_t key = 0u;
+      if (c < m) {
+        const int i = every ? c : c * kK;
+        const int r = br[i];
+        key = r != kEmptyRow && r != kDropRow ? ord_f32(bs[i]) : 0u;
+      }
+      hk[c] = key;
+    }
+    if (tid == 0) lbk_o = 0u;
     __syncthreads();
-    if (w == 0) {
-      WaveList<kK> M;
-      M.init();
+    {
+      uint32_t cand = 0u;
+      const uint4* hk4 = (const uint4*)hk;
 #pragma unroll
-      for (int src = 0; src < 4; ++src) {
-        const bool v = lane < kK && wr[src][lane] != kEmptyRow;
-        M.offer(v ? wk[src][lane] : -__builtin_inff(), v ? wr[src][lane] : kEmptyRow, v);
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t mine = hk[tid + 256 * u];
+        if (mine) {
+          int cnt = 0;
+          for (int i = 0; i < (m + 3) / 4; ++i) {
+            const uint4 v = hk4[i];
+            cnt += (v.x >= mine) + (v.y >= mine) + (v.z >= mine) + (v.w >= mine);
+          }
+          if (cnt >= k_out) cand = max(cand, mine);
+        }
       }
-      const bool have = readlane_i(M.lr, k_out - 1) != kEmptyRow;
-      const float ak = readlane_f(M.ls, k_out - 1);
-      const float c = have ? ak - e2_lds[qi] : -__builtin_inff();
+#pragma unroll
+      for (int off = 32; off; off >>= 1) cand = max(cand, (uint32_t)__shfl_xor((int)cand, off));
+      if (lane == 0 && cand) atomicMax(&lbk_o, cand);
+    }
+    __syncthreads();
+    if (tid == 0) {
       const float dm_all = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-      if (lane == 0) {
-        cut = c;
-        // a dropped row at or above a_k - e2 could belong to the top-k: not proven
-        if (dm_all > -__builtin_inff() && dm_all >= c) fail = 1;
-      }
+      cut = lbk_o ? unord_f32(lbk_o) - e2_lds[qi] : -__builtin_inff();
+      // a dropped row at or above LB - e2 could belong to the top-k: not proven
+      if (dm_all > -__builtin_inff() && dm_all >= cut) fail = 1;
     }
     __syncthreads();
     for (int i = tid; i < n; i += 256) {
@@ -350,14 +388,15 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     __syncthreads();
     if (n_sv > kSurvCap && tid == 0) fail = 1;
     __syncthreads();
-    if (!fail) {
+    if (!fail && !(force & 16)) {
       const int ns = n_sv;
-      // exact re-score: 16 lanes per survivor, 16 survivors per round, every row's loads in flight
+      // exact re-score: 8 lanes per survivor, 32 survivors per round, every row's loads in flight
+      // (a round costs about one memory latency: config 2 has ~2 rounds)
       constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
       constexpr int EPV = 16 / ESZ;
-      constexpr int VPL = D * ESZ / 256;
-      const int grp = tid >> 4, gl = tid & 15;
-      for (int e0 = 0; e0 < ns; e0 += 16) {
+      constexpr int VPL = D * ESZ / 128;
+      const int grp = tid >> 3, gl = tid & 7;
+      for (int e0 = 0; e0 < ns; e0 += 32) {
         const int e = e0 + grp;
         double acc = 0.0;
         if (e < ns) {
@@ -365,8 +404,8 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
           uint4 xv[VPL], yv[VPL];
 #pragma unroll
           for (int u = 0; u < VPL; ++u) {
-            xv[u] = *(const uint4*)((const uint8_t*)X + (int64_t)r * D * ESZ + (int64_t)(gl + 16 * u) * 16);
-            yv[u] = *(const uint4*)((const uint8_t*)Q + (int64_t)qi * D * ESZ + (int64_t)(gl + 16 * u) * 16);
+            xv[u] = *(const uint4*)((const uint8_t*)X + (int64_t)r * D * ESZ + (int64_t)(gl + 8 * u) * 16);
+            yv[u] = *(const uint4*)((const uint8_t*)Q + (int64_t)qi * D * ESZ + (int64_t)(gl + 8 * u) * 16);
           }
 #pragma unroll
           for (int u = 0; u < VPL; ++u)
@@ -374,7 +413,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
             for (int ee = 0; ee < EPV; ++ee) acc += (double)elem<DT>(xv[u], ee) * (double)elem<DT>(yv[u], ee);
         }
 #pragma unroll
-        for (int off = 8; off; off >>= 1) acc += __shfl_xor(acc, off);  // within the 16-lane group
+        for (int off = 4; off; off >>= 1) acc += __shfl_xor(acc, off);  // within the 8-lane group
         if (gl == 0 && e < ns) sx[e] = (float)acc;
       }
       __syncthreads();

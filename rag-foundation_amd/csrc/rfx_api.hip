@@ -473,6 +473,16 @@ int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t
   return RFX_OK;
 }
 
+// RFX_K11_ABLATE (profiling only; wrong results): kernel 11 phase-skip bits 2 (row stream), 4 (query
+// quantiser), 8 (last block's select), 16 (its re-score and rank), 32 (its a_k over the records)
+int k11_ablate() {
+  static const int v = [] {
+    const char* e = getenv("RFX_K11_ABLATE");
+    return e ? (atoi(e) & 62) : 0;
+  }();
+  return v;
+}
+
 // Kernel 11 (k_screen_valu.hip): a few questions (nq <= 8) on an index holding the int8 copy, on a
 // VALU plan with lists of 16 (5 <= k <= 16) — one launch, plus the gated exact one-launch search.
 bool screen_valu_eligible(const Index& ix, const SearchLayout& L, int64_t nq, int k) {
@@ -1158,7 +1168,7 @@ int search_impl(rfx_index_t h, const void* queries_d, int64_t nq, int k, const u
     if ((rc = mark(ev0))) return rc;
     if (rfx::launch_screen_valu(L.vp, ix->scodes, ix->smeta, ix->sstats, (int)ix->rows, ix->dim, ix->dtype, ix->data,
                                 queries_d, (int)nq, row_mask_d, sv, cs, cr, k, out_scores_d, out_rows_d,
-                                ix->screen == 2, st) != 0)
+                                (ix->screen == 2 ? 1 : 0) | k11_ablate(), st) != 0)
       return fail(RFX_EUNSUPPORTED, "two-pass VALU search launch rejected");
     if ((rc = mark(ev1))) return rc;
     // the exact one-launch search, gated on the word the screen's last block wrote
