@@ -1,6 +1,6 @@
 // k10_dbg.hip — DEBUG BUILD ONLY (librfx_dbg.so, `make dbg`): ablations and ring depths of the
 // two-pass scan's int8 screen (k_scan_screen.h MODE bits: 1 no top-k fold, 2 no launder, 4 prefetch
-// distance 1, 8 no corpus stream, 64 store-wide integer fast-path bound, 128 epilogue in place, 256 min-of-KL slot bound, 512 slow path never taken),
+// distance 1, 8 no corpus stream, 64 store-wide integer fast-path bound, 128 epilogue in place, 256 min-of-KL slot bound, 512 slow path never taken, 1024 serial LDS insert),
 // via rfx_dbg_screen_variant; variant = 1000 * RING + MODE (RING in {4, 6, 8, 10, 12}).
 #include "k_scan_screen.h"
 
@@ -40,6 +40,8 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
     RFX_K10V(8, 256)
     RFX_K10V(8, 288)
     RFX_K10V(8, 512)
+    RFX_K10V(8, 1024)
+    RFX_K10V(8, 1056)
     default:
       return -1;
   }

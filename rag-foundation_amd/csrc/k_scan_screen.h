@@ -116,7 +116,12 @@ __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b)
 // Fold one tile's 16 values of this lane (rows rbase + (r & 7) + 16 (r >> 3), ROWMAP 1 of
 // k_mfma_common.h) into its list.  thr_o: the pruning bound (orderable A, 0 = none); rows are
 // looked at from thr − e2 on.  drop_o: the best A this lane looked at and did not keep.
-template <int KL>
+// Production: the 16 pass tests make a bit mask first; the list is read into registers once (KL
+// independent LDS reads), each lane bubbles its passing values in one per trip (KL compare-exchanges,
+// no memory on the way), and the list is written back once.  The serial LDS insert (one dependent
+// LDS round trip per shifted entry) is debug MODE 1024: a wave in this slow path holds the whole
+// workgroup at the next stage barrier.
+template <int KL, bool REG = true>
 __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint32_t bits, uint64_t* Ls, uint32_t& thr_o,
                                             float e2, uint32_t& drop_o, int rbase, v4i32 tau_rsrc, uint32_t slot_voff) {
   int mx = max3i(a[0][0], a[0][1], a[0][2]);
@@ -129,30 +134,82 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
   mx = max(mx, a[3][3]);
   const float thr = thr_o ? unord(thr_o) - e2 : -__builtin_inff();
   if ((float)mx * st >= thr) {  // s_t >= 0: the tile's best A bounds every row's
+    if constexpr (REG) {
+      // which of the 16 values pass, without branching on each one
+      uint32_t pm = 0;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float s = (float)a[r >> 2][r & 3] * st;
-      if (((bits >> ((r & 7) + 16 * (r >> 3))) & 1u) && s >= thr) {
+      for (int r = 0; r < 16; ++r) {
+        const float s = (float)a[r >> 2][r & 3] * st;
+        const bool on = ((bits >> ((r & 7) + 16 * (r >> 3))) & 1u) && s >= thr;
+        pm |= on ? (1u << r) : 0u;
+      }
+      uint64_t L[KL];
+#pragma unroll
+      for (int i = 0; i < KL; ++i) L[i] = Ls[i * 64];
+      // one passing value per lane per trip: the wave makes max-over-lanes(popcount) trips, not one
+      // trip per position some lane passes at
+      while (pm) {
+        const int r = __builtin_ctz(pm);
+        pm &= pm - 1;
+        // value r: a select tree on r's bits as bit-field inserts (15 v_bfi_b32); the masks go through
+        // an empty asm so the compiler cannot turn the tree back into an indexed (scratch) read of a
+        int m3 = -((r >> 3) & 1), m2 = -((r >> 2) & 1), m1 = -((r >> 1) & 1), m0 = -(r & 1);
+        asm volatile("" : "+v"(m3), "+v"(m2), "+v"(m1), "+v"(m0));
+        int v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = (a[(j + 8) >> 2][j & 3] & m3) | (a[j >> 2][j & 3] & ~m3);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = (v[j + 4] & m2) | (v[j] & ~m2);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) v[j] = (v[j + 2] & m1) | (v[j] & ~m1);
+        const int av = (v[1] & m0) | (v[0] & ~m0);
+        const float s = (float)av * st;
         const int row = rbase + (r & 7) + 16 * (r >> 3);
         const uint64_t key = ((uint64_t)ord(s) << 32) | (uint32_t)(~(uint32_t)row);
-        const uint64_t last = Ls[(KL - 1) * 64];
-        if (key > last) {
-          if (last) drop_o = max(drop_o, (uint32_t)(last >> 32));  // evicted
-          int i = KL - 1;
-          for (; i > 0; --i) {
-            const uint64_t prev = Ls[(i - 1) * 64];
-            if (prev >= key) break;
-            Ls[i * 64] = prev;
+        if (key > L[KL - 1]) {
+          if (L[KL - 1]) drop_o = max(drop_o, (uint32_t)(L[KL - 1] >> 32));  // evicted
+          uint64_t k = key;
+#pragma unroll
+          for (int i = 0; i < KL; ++i) {  // bubble: L stays sorted, the smallest falls out
+            const uint64_t hi = L[i] > k ? L[i] : k;
+            k = L[i] > k ? k : L[i];
+            L[i] = hi;
           }
-          Ls[i * 64] = key;
         } else {
           drop_o = max(drop_o, ord(s));  // looked at, not kept
         }
       }
+#pragma unroll
+      for (int i = 0; i < KL; ++i) Ls[i * 64] = L[i];
+      const uint32_t own = (uint32_t)(L[KL - 1] >> 32);
+      thr_o = own > thr_o ? own : thr_o;
+      batomic_umax(tau_rsrc, slot_voff, (uint32_t)(L[0] >> 32));
+    } else {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float s = (float)a[r >> 2][r & 3] * st;
+        if (((bits >> ((r & 7) + 16 * (r >> 3))) & 1u) && s >= thr) {
+          const int row = rbase + (r & 7) + 16 * (r >> 3);
+          const uint64_t key = ((uint64_t)ord(s) << 32) | (uint32_t)(~(uint32_t)row);
+          const uint64_t last = Ls[(KL - 1) * 64];
+          if (key > last) {
+            if (last) drop_o = max(drop_o, (uint32_t)(last >> 32));  // evicted
+            int i = KL - 1;
+            for (; i > 0; --i) {
+              const uint64_t prev = Ls[(i - 1) * 64];
+              if (prev >= key) break;
+              Ls[i * 64] = prev;
+            }
+            Ls[i * 64] = key;
+          } else {
+            drop_o = max(drop_o, ord(s));  // looked at, not kept
+          }
+        }
+      }
+      const uint32_t own = (uint32_t)(Ls[(KL - 1) * 64] >> 32);
+      thr_o = own > thr_o ? own : thr_o;
+      batomic_umax(tau_rsrc, slot_voff, (uint32_t)(Ls[0] >> 32));
     }
-    const uint32_t own = (uint32_t)(Ls[(KL - 1) * 64] >> 32);
-    thr_o = own > thr_o ? own : thr_o;
-    batomic_umax(tau_rsrc, slot_voff, (uint32_t)(Ls[0] >> 32));
   }
 }
 
@@ -167,7 +224,8 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
 // wave's first query), 64 = the fast path on the store-wide integer bound (max tile scale) instead
 // of the tile's own scale, 128 = the epilogue in place at each tile's end (no alternating accumulators),
 // 256 = kernel 6's slot-table bound (min over KL slots) instead of the KL-th largest of 16, 512 = the
-// slow path compiled in but never taken (wrong results; separates its cost from the code's presence).
+// slow path compiled in but never taken (wrong results; separates its cost from the code's presence),
+// 1024 = the slow path's serial LDS list insert instead of the register-resident list.
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
@@ -369,7 +427,8 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
             acc4[2 * rb][i] = (int)r[0];
             acc4[2 * rb + 1][i] = (int)r[1];
           }
-        fold_screen<KL>(acc4, st, lw >> (8 * half), Ls, thr, e2, drop, tile * kTM + 8 * half, tau_rsrc, slot_voff);
+        fold_screen<KL, (MODE & 1024) == 0>(acc4, st, lw >> (8 * half), Ls, thr, e2, drop, tile * kTM + 8 * half,
+                                            tau_rsrc, slot_voff);
         set_bounds();
       }
     } else if (hit && m0 == 12345 && m1 == 54321) {
