@@ -319,7 +319,7 @@ def main():
         alg_bytes = n_max * a.dim * esz + a.nq * a.dim * esz + a.nq * a.k * 12
     achieved = alg_bytes / (scan_ms * 1e-3) / 1e9
     qps = a.nq * a.steps / elapsed
-    workload_key = f"{a.rows}x{a.dim}-{a.dtype}-nq{a.nq}-k{a.k}-g{world}" + ("-screen" if kern == 10 else "")
+    workload_key = f"{a.rows}x{a.dim}-{a.dtype}-nq{a.nq}-k{a.k}-g{world}" + ("-screen" if kern in (10, 11) else "")
     result = {
         "metric": METRIC,
         "value": round(qps, 1),

@@ -106,3 +106,56 @@ def test_cfg5_recall_vs_oracle_bruteforce(cfg5):
     # in lists outside the 32 probed (a quality property of IVF, not a parity one); the floor below
     # catches a broken probe / list build, which drops recall far lower
     assert rec(r_ivf) >= 0.8 and rec(r_rr) >= rec(r_ivf), (rec(r_ivf), rec(r_rr))
+
+
+@pytest.mark.timeout(600)
+def test_cfg5_through_ivf_store(cfg5, tmp_path):
+    """The same shape served from an RFX_INDEX=ivf store (rfx/store.py): four
+    uploads of 2^18 rows, the writer trains at the fourth (train_min = N) on its strided sample of
+    the live rows (262,144 rows, 10 iterations).  The committed centroids equal an IvfIndex trained
+    on the same rows (the trainer itself is held to the oracle above); the store's answers (nprobe 32,
+    exact re-rank of 20 candidates against the DeviceIndex rows in place) are bit-identical to
+    IvfIndex.search_rerank over the same lists, every score is the f64 dot of its stored row within
+    1e-5, and recall@10 against the oracle's brute force is at least the list search's."""
+    import os
+    from rfx import store as rstore
+    from rfx.ivf import IvfIndex
+    rows, rows_np, q = cfg5["rows"], cfg5["rows_np"], cfg5["q"]
+    reg = rstore.StoreRegistry(root=str(tmp_path), device=0)
+    st = reg.create("cfg5", DIM, "bf16", spec={"kind": "ivf", "nlist": NLIST, "nprobe": NPROBE, "train_min": N})
+    part = N // 4
+    for i in range(4):
+        st.add_document([f"c{j}" for j in range(part)], rows[i * part:(i + 1) * part], f"part{i}.md")
+        assert st.ivf_ready() == (i == 3)
+    sample = np.arange(N)[::max(1, N // (64 * NLIST))]
+    ref = IvfIndex(DIM, NLIST)
+    ref.train(rows[torch.from_numpy(sample).cuda()].contiguous(), iters=10)
+    raw = open(os.path.join(st.path, f"ivf-{st.ivf_id}.bin"), "rb").read()
+    assert raw[20:] == ref.centroid_bytes(), "store centroids differ from the same training"
+    ref.add(rows)
+    ref.build()
+    s, r = st.search(q, K)
+    rs, rr = ref.search_rerank(q, K, NPROBE, rows, rerank_k=2 * K)
+    assert np.array_equal(r.numpy(), rr.cpu().numpy()), "store rows differ from the list search"
+    assert np.array_equal(s.numpy().view(np.uint32), rs.cpu().numpy().view(np.uint32))
+    s, r = s.numpy(), r.numpy()
+    q64 = osynth.to_f64(to_np(q), "bf16")
+    for i in range(0, NQ, 8):
+        ok = r[i] >= 0
+        exact = osynth.to_f64(rows_np[r[i][ok]], "bf16") @ q64[i]
+        assert np.all(np.abs(s[i][ok] - exact) <= 1e-5) and np.all(np.diff(s[i][ok]) <= 0)
+    sel = np.arange(0, NQ, 4)
+
+    def blocks():
+        for b in range(0, N, BLK):
+            yield b, oivf.stored_to_f32(rows_np[b:b + BLK], "bf16")
+
+    _, exact = osearch.topk_blocks(q64[sel], blocks(), K)
+    rec = float(np.mean([len(set(r[i].tolist()) & set(exact[j].tolist())) / K for j, i in enumerate(sel)]))
+    _, r_ivf = ref.search(q, K, NPROBE)
+    r_ivf = r_ivf.cpu().numpy()
+    rec_ivf = float(np.mean([len(set(r_ivf[i].tolist()) & set(exact[j].tolist())) / K for j, i in enumerate(sel)]))
+    print(f"cfg5 store recall@{K}: {rec:.4f} (list search {rec_ivf:.4f})")
+    assert rec >= 0.85 and rec >= rec_ivf, (rec, rec_ivf)
+    ref.close()
+    reg.drop(st.name)
