@@ -37,10 +37,12 @@ MfmaPlan plan_scan_mfma6(int64_t nrows, int D, int dtype, int64_t nq, int k) {
 }
 
 int launch_scan_mfma6(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask, const uint32_t* gate) {
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask, const uint32_t* gate,
+                      bool tau_zeroed) {
+  static_assert(k6::kTauW == kFallbackTauW, "screen_queries_kernel zeroes this table for the gated fallback");
   if (!p.ok || D != 768) return -1;
   const int ntiles = (nrows + k6::kTM - 1) / k6::kTM;
-  if (hipMemsetAsync(tau, 0, tau_bytes_mfma6(p), st) != hipSuccess) return -2;
+  if (!tau_zeroed && hipMemsetAsync(tau, 0, tau_bytes_mfma6(p), st) != hipSuccess) return -2;
   dim3 grid(p.blocks, p.q_blocks);
   auto f = dtype == RFX_BF16 ? k6::launch_bf16_768 : k6::launch_f16_768;
   return f(p.k_lane, grid, st, (const uint16_t*)X, (const uint16_t*)Qpad, nq, ntiles, tau, cs, cr, p.n_lists, mask, gate);

@@ -38,10 +38,12 @@ MfmaPlan plan_scan_mfma8(int64_t nrows, int D, int dtype, int64_t nq, int k) {
 }
 
 int launch_scan_mfma8(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask, const uint32_t* gate) {
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask, const uint32_t* gate,
+                      bool tau_zeroed) {
+  static_assert(k8::kTauW == kFallbackTauW, "screen_queries_kernel zeroes this table for the gated fallback");
   if (!p.ok || D != 1024) return -1;
   const int ntiles = (nrows + k8::kTM - 1) / k8::kTM;
-  if (hipMemsetAsync(tau, 0, tau_bytes_mfma8(p), st) != hipSuccess) return -2;
+  if (!tau_zeroed && hipMemsetAsync(tau, 0, tau_bytes_mfma8(p), st) != hipSuccess) return -2;
   const int paired = p.blocks % 8 == 0 ? 1 : 0;
   dim3 grid(p.blocks * p.q_blocks);
   auto f = dtype == RFX_BF16 ? k8::launch_bf16_1024 : k8::launch_f16_1024;

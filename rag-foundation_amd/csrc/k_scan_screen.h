@@ -135,14 +135,12 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
   const float thr = thr_o ? unord(thr_o) - e2 : -__builtin_inff();
   if ((float)mx * st >= thr) {  // s_t >= 0: the tile's best A bounds every row's
     if constexpr (REG) {
-      // which of the 16 values pass, without branching on each one
+      // which of the 16 values pass (live bits applied once, re-ordered to r: bit r <- row bit
+      // (r & 7) + 16 (r >> 3)), without branching on each one
       uint32_t pm = 0;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float s = (float)a[r >> 2][r & 3] * st;
-        const bool on = ((bits >> ((r & 7) + 16 * (r >> 3))) & 1u) && s >= thr;
-        pm |= on ? (1u << r) : 0u;
-      }
+      for (int r = 0; r < 16; ++r) pm |= (float)a[r >> 2][r & 3] * st >= thr ? (1u << r) : 0u;
+      pm &= (bits & 0xffu) | ((bits >> 8) & 0xff00u);
       uint64_t L[KL];
 #pragma unroll
       for (int i = 0; i < KL; ++i) L[i] = Ls[i * 64];
@@ -165,19 +163,21 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
         const int av = (v[1] & m0) | (v[0] & ~m0);
         const float s = (float)av * st;
         const int row = rbase + (r & 7) + 16 * (r >> 3);
+        // insert, unconditionally and without a dependency chain: with c_i = (L_i > key) and the list
+        // sorted, the new entry i is c_{i-1} ? (c_i ? L_i : key) : L_{i-1} (c_{-1} = true), and the
+        // smallest of L and the key falls out — the evicted entry when the key goes in, the key itself
+        // when it does not; either way a value this lane looked at and did not keep (an empty entry
+        // falls out as 0, which max ignores).  KL independent compares, no branch: the list stays in
+        // the same registers from trip to trip.
         const uint64_t key = ((uint64_t)ord(s) << 32) | (uint32_t)(~(uint32_t)row);
-        if (key > L[KL - 1]) {
-          if (L[KL - 1]) drop_o = max(drop_o, (uint32_t)(L[KL - 1] >> 32));  // evicted
-          uint64_t k = key;
+        bool c[KL];
 #pragma unroll
-          for (int i = 0; i < KL; ++i) {  // bubble: L stays sorted, the smallest falls out
-            const uint64_t hi = L[i] > k ? L[i] : k;
-            k = L[i] > k ? k : L[i];
-            L[i] = hi;
-          }
-        } else {
-          drop_o = max(drop_o, ord(s));  // looked at, not kept
-        }
+        for (int i = 0; i < KL; ++i) c[i] = L[i] > key;
+        const uint64_t k = c[KL - 1] ? key : L[KL - 1];
+#pragma unroll
+        for (int i = KL - 1; i > 0; --i) L[i] = c[i - 1] ? (c[i] ? L[i] : key) : L[i - 1];
+        L[0] = c[0] ? L[0] : key;
+        drop_o = max(drop_o, (uint32_t)(k >> 32));
       }
 #pragma unroll
       for (int i = 0; i < KL; ++i) Ls[i * 64] = L[i];

@@ -159,13 +159,15 @@ template <int DT, int D>
 __global__ __launch_bounds__(256) void screen_queries_kernel(const uint16_t* __restrict__ Q, int nq, int nq_pad,
                                                              int8_t* __restrict__ Qc, float* __restrict__ qe2,
                                                              const uint32_t* __restrict__ stats,
-                                                             uint32_t* __restrict__ tau, uint32_t* __restrict__ gate) {
+                                                             uint32_t* __restrict__ tau, uint32_t* __restrict__ gate,
+                                                             uint32_t* __restrict__ ftau) {
   constexpr int NM = D / 256;
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x == 0) *gate = 0u;
   if (q >= nq_pad) return;
   if (lane < k10::kTauW) tau[(int64_t)q * k10::kTauW + lane] = 0u;
+  if (ftau && lane < kFallbackTauW) ftau[(int64_t)q * kFallbackTauW + lane] = 0u;  // the gated fallback's table
   float y[NM][4];
   float am = 0.f;
 #pragma unroll
@@ -226,7 +228,10 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
                                                             float* __restrict__ out_s, int64_t* __restrict__ out_r,
                                                             Rec* __restrict__ out_rec, uint32_t* __restrict__ gate,
                                                             int* __restrict__ diag, int force) {
-  constexpr int NT = 512, NW = NT / 64, NM = D / 256, U = 4;
+  // U1: candidate entries per thread per round (config 3: 512 lists x 10 = 5,120 = one round, rows
+  // loaded with the scores, and the drops with them: one memory round trip instead of four);
+  // U: survivor rows per wave per round of the exact re-score
+  constexpr int NT = 512, NW = NT / 64, NM = D / 256, U = 8, U1 = 10;
   __shared__ float ca[kSelCap];   // screen score A of kept candidate i
   __shared__ int crow[kSelCap];   // its row
   __shared__ int sv[kSelCap];     // survivor j -> candidate index
@@ -244,17 +249,23 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
   const int64_t n = n_lists * list_len;
   const float* qs = cs + q * n;
   const int* qr = cr + q * n;
-  for (int64_t b = tid; b < n; b += (int64_t)NT * U) {
-    float s[U];
+  const uint32_t d0 = tid < n_lists ? drops[q * n_lists + tid] : 0u;  // step 3's, loaded now
+  for (int64_t b = tid; b < n; b += (int64_t)NT * U1) {
+    float s[U1];
+    int r[U1];
 #pragma unroll
-    for (int u = 0; u < U; ++u) s[u] = b + u * NT < n ? qs[b + u * NT] : -__builtin_inff();
+    for (int u = 0; u < U1; ++u) {
+      const bool in = b + u * NT < n;
+      s[u] = in ? qs[b + u * NT] : -__builtin_inff();
+      r[u] = in ? qr[b + u * NT] : 0;
+    }
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U1; ++u)
       if (s[u] != -__builtin_inff()) {
         const int i = atomicAdd(&n_c, 1);
         if (i < kSelCap) {
           ca[i] = s[u];
-          crow[i] = qr[b + u * NT];
+          crow[i] = r[u];
         }
       }
   }
@@ -278,7 +289,8 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
   const float t = ncl >= k ? ak - e2 : -__builtin_inff();
   const uint32_t ot = ord(t);
   // 3. a row dropped at or above t could be a survivor the lists lost: fallback
-  for (int64_t j = tid; j < n_lists; j += NT) {
+  if (d0 && d0 >= ot) fail = 1;
+  for (int64_t j = tid + NT; j < n_lists; j += NT) {
     const uint32_t d = drops[q * n_lists + j];
     if (d && d >= ot) fail = 1;
   }
@@ -419,11 +431,11 @@ MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k) {
 size_t tau_bytes_screen(const MfmaPlan& p) { return (size_t)p.nq_pad * k10::kTauW * sizeof(uint32_t); }
 
 void launch_screen_queries(const void* Q, int dtype, int D, int64_t nq, int64_t nq_pad, int8_t* Qc, float* qe2,
-                           const uint32_t* stats, uint32_t* tau, uint32_t* gate, hipStream_t st) {
+                           const uint32_t* stats, uint32_t* tau, uint32_t* gate, uint32_t* ftau, hipStream_t st) {
   const dim3 grid((unsigned)((nq_pad + 3) / 4));
 #define RFX_SQQ(DTV, DV)                                                                                       \
   hipLaunchKernelGGL((screen_queries_kernel<DTV, DV>), grid, dim3(256), 0, st, (const uint16_t*)Q, (int)nq,      \
-                     (int)nq_pad, Qc, qe2, stats, tau, gate)
+                     (int)nq_pad, Qc, qe2, stats, tau, gate, ftau)
   if (dtype == RFX_BF16 && D == 768)
     RFX_SQQ(RFX_BF16, 768);
   else if (dtype == RFX_BF16)

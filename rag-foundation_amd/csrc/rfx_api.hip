@@ -443,7 +443,12 @@ int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t
   uint32_t* drops = (uint32_t*)(ws + L.s_drop);
   uint32_t* gate = (uint32_t*)(ws + L.s_gate);
   int* diag = (int*)(ws + L.s_diag);
-  rfx::launch_screen_queries(queries, ix.dtype, ix.dim, nq, L.sp.nq_pad, qc, qe2, ix.sstats, stau, gate, st);
+  uint32_t* tau = (uint32_t*)(ws + L.tau_off);
+  // the fallback's threshold table is zeroed by the query quantiser when it covers the fallback's
+  // padded batch (kernel 10 pads to 256 queries, kernels 6 / 8 to 256 / 128): no memset launch
+  const bool ftau = L.mp.nq_pad <= L.sp.nq_pad;
+  rfx::launch_screen_queries(queries, ix.dtype, ix.dim, nq, L.sp.nq_pad, qc, qe2, ix.sstats, stau, gate,
+                             ftau ? tau : nullptr, st);
   if (ev0) RFX_HIP(hipEventRecord((hipEvent_t)ev0, st));
   if (rfx::launch_scan_screen(L.sp, ix.scodes, ix.smeta, ix.sstats, (int)ix.rows, ix.dim, qc, qe2, (int)nq, stau, scs,
                               scr, drops, st, mask) != 0)
@@ -458,13 +463,12 @@ int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t
     qpad = ws + L.q_off;
     rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, 2, (void*)qpad, st);
   }
-  uint32_t* tau = (uint32_t*)(ws + L.tau_off);
   float* cs = (float*)(ws + L.cs_off);
   int32_t* cr = (int32_t*)(ws + L.cr_off);
   const int rc = L.fbk == 6 ? rfx::launch_scan_mfma6(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs,
-                                                     cr, st, mask, gate)
+                                                     cr, st, mask, gate, ftau)
                             : rfx::launch_scan_mfma8(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs,
-                                                     cr, st, mask, gate);
+                                                     cr, st, mask, gate, ftau);
   if (rc != 0) return fail(RFX_EUNSUPPORTED, "fallback scan launch rejected (%d)", rc);
   if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.n_cand, L.mp.k_lane, k, row_offset, out_rec ? nullptr : out_s,
                                    out_rec ? nullptr : out_r, out_rec, st, /*sorted=*/true, gate) != 0)
@@ -1085,7 +1089,7 @@ int rfx_dbg_screen_variant(rfx_index_t h, const void* queries_d, int64_t nq, int
   float* qe2 = (float*)(ws + L.s_qe2);
   uint32_t* stau = (uint32_t*)(ws + L.s_tau);
   rfx::launch_screen_queries(queries_d, ix->dtype, ix->dim, nq, L.sp.nq_pad, qc, qe2, ix->sstats, stau,
-                             (uint32_t*)(ws + L.s_gate), st);
+                             (uint32_t*)(ws + L.s_gate), nullptr, st);
   if (rfx::launch_scan_screen_dbg(L.sp, variant, ix->scodes, ix->smeta, ix->sstats, (int)ix->rows, qc, qe2, (int)nq, stau,
                                   (float*)(ws + L.s_cs), (int*)(ws + L.s_cr), (uint32_t*)(ws + L.s_drop), st) != 0)
     return fail(RFX_EUNSUPPORTED, "screen variant %d unsupported", variant);

@@ -96,7 +96,7 @@ MfmaPlan plan_scan_mfma6(int64_t nrows, int D, int dtype, int64_t nq, int k);
 // the two-pass scan runs only when the screen's select kernel asked for it)
 int launch_scan_mfma6(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
                       uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr,
-                      const uint32_t* gate = nullptr);
+                      const uint32_t* gate = nullptr, bool tau_zeroed = false);
 int launch_scan_mfma6_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, int dtype, const void* Qpad, int nq,
                           uint32_t* tau, float* cs, int* cr, hipStream_t st);
 size_t tau_bytes_mfma7(const MfmaPlan& p);
@@ -107,7 +107,7 @@ size_t tau_bytes_mfma8(const MfmaPlan& p);
 MfmaPlan plan_scan_mfma8(int64_t nrows, int D, int dtype, int64_t nq, int k);
 int launch_scan_mfma8(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
                       uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr,
-                      const uint32_t* gate = nullptr);
+                      const uint32_t* gate = nullptr, bool tau_zeroed = false);
 // f32 stores (kernel 9): batched scan on v_mfma_f32_16x16x4_f32 for 16 < nq
 size_t tau_bytes_mfma9(const MfmaPlan& p);
 MfmaPlan plan_scan_mfma9(int64_t nrows, int D, int dtype, int64_t nq, int k);
@@ -134,8 +134,11 @@ void launch_screen_quantize(const void* X, int D, int dtype, int64_t tile0, int6
                             int8_t* codes, void* tmeta, uint32_t* stats, hipStream_t st);
 MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k);
 size_t tau_bytes_screen(const MfmaPlan& p);
+// ftau (or null): the gated fallback scan's threshold table ([nq_pad][kFallbackTauW], kernel 6 / 8),
+// zeroed here so the fallback launch needs no memset of its own (tau_zeroed below)
+constexpr int kFallbackTauW = 16;
 void launch_screen_queries(const void* Q, int dtype, int D, int64_t nq, int64_t nq_pad, int8_t* Qc, float* qe2,
-                           const uint32_t* stats, uint32_t* tau, uint32_t* gate, hipStream_t st);
+                           const uint32_t* stats, uint32_t* tau, uint32_t* gate, uint32_t* ftau, hipStream_t st);
 int launch_scan_screen(const MfmaPlan& p, const int8_t* codes, const void* tmeta, const uint32_t* stats, int nrows, int D,
                        const int8_t* Qc, const float* qe2, int nq, uint32_t* tau, float* cs, int* cr, uint32_t* drops,
                        hipStream_t st, const uint32_t* mask);
