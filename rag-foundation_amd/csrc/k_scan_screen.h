@@ -116,13 +116,13 @@ __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b)
 // Fold one tile's 16 values of this lane (rows rbase + (r & 7) + 16 (r >> 3), ROWMAP 1 of
 // k_mfma_common.h) into its list.  thr_o: the pruning bound (orderable A, 0 = none); rows are
 // looked at from thr − e2 on.  drop_o: the best A this lane looked at and did not keep.
-// Production: the 16 pass tests make a bit mask first; the list is read into registers once (KL
-// independent LDS reads), each lane bubbles its passing values in one per trip (KL compare-exchanges,
-// no memory on the way), and the list is written back once.  The serial LDS insert (one dependent
+// Production: the 16 pass tests make a bit mask first; the list (L) lives in registers for the whole
+// scan, and each lane inserts its passing values one per trip (KL independent compares, no memory).  The serial LDS insert (one dependent
 // LDS round trip per shifted entry) is debug MODE 1024: a wave in this slow path holds the whole
 // workgroup at the next stage barrier.
 template <int KL, bool REG = true>
-__device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint32_t bits, uint64_t* Ls, uint32_t& thr_o,
+__device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint32_t bits, uint64_t* Ls, uint64_t (&L)[KL],
+                                            uint32_t& thr_o,
                                             float e2, uint32_t& drop_o, int rbase, v4i32 tau_rsrc, uint32_t slot_voff) {
   int mx = max3i(a[0][0], a[0][1], a[0][2]);
   mx = max3i(mx, a[0][3], a[1][0]);
@@ -141,9 +141,6 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
 #pragma unroll
       for (int r = 0; r < 16; ++r) pm |= (float)a[r >> 2][r & 3] * st >= thr ? (1u << r) : 0u;
       pm &= (bits & 0xffu) | ((bits >> 8) & 0xff00u);
-      uint64_t L[KL];
-#pragma unroll
-      for (int i = 0; i < KL; ++i) L[i] = Ls[i * 64];
       // one passing value per lane per trip: the wave makes max-over-lanes(popcount) trips, not one
       // trip per position some lane passes at
       while (pm) {
@@ -179,8 +176,6 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
         L[0] = c[0] ? L[0] : key;
         drop_o = max(drop_o, (uint32_t)(k >> 32));
       }
-#pragma unroll
-      for (int i = 0; i < KL; ++i) Ls[i * 64] = L[i];
       const uint32_t own = (uint32_t)(L[KL - 1] >> 32);
       thr_o = own > thr_o ? own : thr_o;
       batomic_umax(tau_rsrc, slot_voff, (uint32_t)(L[0] >> 32));
@@ -263,9 +258,12 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
 #pragma unroll
     for (int i = 0; i < kTauBytes / 16 / 512; ++i) tz[tid + 512 * i] = uint4{0u, 0u, 0u, 0u};
   }
-  uint64_t* const Ls = (uint64_t*)(lds + kListOff) + (w * KL) * 64 + lane;
+  uint64_t* const Ls = (uint64_t*)(lds + kListOff) + (w * KL) * 64 + lane;  // debug MODE 1024's list
 #pragma unroll
   for (int i = 0; i < KL; ++i) Ls[i * 64] = 0ull;
+  uint64_t Lr[KL];  // production: the lane's list lives in registers for the whole scan
+#pragma unroll
+  for (int i = 0; i < KL; ++i) Lr[i] = 0ull;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -427,7 +425,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
             acc4[2 * rb][i] = (int)r[0];
             acc4[2 * rb + 1][i] = (int)r[1];
           }
-        fold_screen<KL, (MODE & 1024) == 0>(acc4, st, lw >> (8 * half), Ls, thr, e2, drop, tile * kTM + 8 * half,
+        fold_screen<KL, (MODE & 1024) == 0>(acc4, st, lw >> (8 * half), Ls, Lr, thr, e2, drop, tile * kTM + 8 * half,
                                             tau_rsrc, slot_voff);
         set_bounds();
       }
@@ -541,7 +539,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
     const int64_t o = ((int64_t)q * n_lists + lst) * KL;
 #pragma unroll
     for (int i = 0; i < KL; ++i) {
-      const uint64_t key = Ls[i * 64];
+      const uint64_t key = (MODE & 1024) == 0 ? Lr[i] : Ls[i * 64];
       const float sc = unord((uint32_t)(key >> 32));
       const bool keep = key && sc >= lo;
       cand_s[o + i] = keep ? sc : -__builtin_inff();

@@ -236,6 +236,7 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
   __shared__ int crow[kSelCap];   // its row
   __shared__ int sv[kSelCap];     // survivor j -> candidate index
   __shared__ double sx[kSelCap];  // survivor j's exact score
+  __shared__ int srow[kSelCap];   // survivor j's row (the rank loop reads it without the sv -> crow hop)
   __shared__ int n_c, n_sv, n_ok, fail;
   __shared__ float ak;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
@@ -277,6 +278,7 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
   for (int i = tid; i < ncl; i += NT) {
     const float si = ca[i];
     int gt = 0, ge = 0;
+#pragma unroll 8
     for (int j = 0; j < ncl; ++j) {
       const float sj = ca[j];
       gt += sj > si;
@@ -338,7 +340,10 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
 #pragma unroll
       for (int off = 32; off; off >>= 1) acc += __shfl_xor(acc, off);
       const int j = j0 + u * NW;
-      if (lane == 0 && j < ns) sx[j] = acc;
+      if (lane == 0 && j < ns) {
+        sx[j] = acc;
+        srow[j] = crow[sv[j]];
+      }
     }
   }
   __syncthreads();
@@ -346,11 +351,12 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
   for (int j = tid; j < ns; j += NT) {
     const double sj = sx[j];
     if (sj != sj) continue;
-    const int rj = crow[sv[j]];
+    const int rj = srow[j];
     int rank = 0;
+#pragma unroll 8
     for (int i = 0; i < ns; ++i) {
       const double si = sx[i];
-      rank += si > sj || (si == sj && crow[sv[i]] < rj);
+      rank += si > sj || (si == sj && srow[i] < rj);
     }
     atomicAdd(&n_ok, 1);
     if (rank < k) {
