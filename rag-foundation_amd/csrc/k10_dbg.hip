@@ -1,6 +1,8 @@
 // k10_dbg.hip — DEBUG BUILD ONLY (librfx_dbg.so, `make dbg`): ablations and ring depths of the
 // two-pass scan's int8 screen (k_scan_screen.h MODE bits: 1 no top-k fold, 2 no launder, 4 prefetch
-// distance 1, 8 no corpus stream, 64 store-wide integer fast-path bound, 128 epilogue in place, 256 min-of-KL slot bound, 512 slow path never taken, 1024 serial LDS insert),
+// distance 1, 8 no corpus stream, 16 early slot-table refreshes, 32 slow-path entry count, 64 store-wide
+// integer fast-path bound, 128 epilogue in place, 256 min-of-KL slot bound, 512 slow path never taken,
+// 1024 serial LDS insert),
 // via rfx_dbg_screen_variant; variant = 1000 * RING + MODE (RING in {4, 6, 8, 10, 12}).
 #include "k_scan_screen.h"
 
@@ -42,6 +44,8 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
     RFX_K10V(8, 512)
     RFX_K10V(8, 1024)
     RFX_K10V(8, 1056)
+    RFX_K10V(8, 16)
+    RFX_K10V(8, 48)
     default:
       return -1;
   }

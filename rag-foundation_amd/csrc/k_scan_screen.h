@@ -68,7 +68,12 @@ constexpr int lds_bytes() { return list_off<RING>() + kWaves * KL * 64 * 8; }
 static_assert(lds_bytes<10, 12>() <= 163840, "LDS budget");
 static_assert(kSlot / 1024 == kWaves * kGPW && kTauGPW == 2, "DMA pieces per wave");
 
-__device__ __forceinline__ bool tau_refresh_tile(int it) { return it < 2 || (it & 3) == 3; }
+// the slot table is re-read at the end of these tiles (used two tiles later); debug MODE 16: at every one
+// of the first 16 tiles (the bound's warm-up), then every 4th
+template <int MODE>
+__device__ __forceinline__ bool tau_refresh_tile(int it) {
+  return it < ((MODE & 16) != 0 ? 16 : 2) || (it & 3) == 3;
+}
 
 // The pruning bound from a query's kTauW = 16 slots: list j publishes its best A to slot j % 16, so
 // the slots hold the A of 16 distinct rows (lists are disjoint row sets) and the KL-th largest slot is
@@ -220,7 +225,8 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
 // of the tile's own scale, 128 = the epilogue in place at each tile's end (no alternating accumulators),
 // 256 = kernel 6's slot-table bound (min over KL slots) instead of the KL-th largest of 16, 512 = the
 // slow path compiled in but never taken (wrong results; separates its cost from the code's presence),
-// 1024 = the slow path's serial LDS list insert instead of the register-resident list.
+// 1024 = the slow path's serial LDS list insert instead of the register-resident list, 16 = the slot
+// table re-read at every one of the first 16 tiles.
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
@@ -435,7 +441,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   };
   auto tile_body = [&](const int it, v4i32(&acc4)[4], v4i32(&accp)[4], const bool prev) {
     const int gbase = it * NST;
-    if (it >= 2 && tau_refresh_tile(it - 2)) {
+    if (it >= 2 && tau_refresh_tile<MODE>(it - 2)) {
       thr = max(thr, (MODE & 256) != 0 ? tau_min<KL>(tq) : tau_kth<KL>(tq));
       set_bounds();
     }
@@ -451,7 +457,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
       const int dmax = (RING - 3 + NST - s) / NST;
       bool y = false;
 #pragma unroll
-      for (int d = 1; d <= dmax; ++d) y = y || (it >= d && tau_refresh_tile(it - d));
+      for (int d = 1; d <= dmax; ++d) y = y || (it >= d && tau_refresh_tile<MODE>(it - d));
       return y;
     };
 #pragma unroll
@@ -483,7 +489,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
           }
           asm volatile("s_barrier" ::: "memory");
           if constexpr ((MODE & 8) == 0)
-            if (s == NST - 1 && tau_refresh_tile(it)) issue_tau();
+            if (s == NST - 1 && tau_refresh_tile<MODE>(it)) issue_tau();
         }
         const int ks = s * KPS + kk;
         fr[(ks + PF) % NF] = kk + PF < KPS ? read_frag(slot, kk + PF) : read_frag((g + 1) % RING, kk + PF - KPS);
