@@ -144,6 +144,7 @@ def main():
         dist.init_process_group("gloo")  # control plane only (bootstrap, barriers, timing)
 
     from rfx import dist as rdist
+    from rfx._lib import RfxCapacityError
     from rfx.index import DeviceIndex, merge_gathered, synth_rows
 
     comm, exchange_note = None, None
@@ -182,16 +183,25 @@ def main():
     copies = a.copies or min(8, max(1, -(-(768 << 20) // max(n_local * row_bytes, 1)) + 1))
     if copies > 1 and n_local * row_bytes > (1 << 30):
         copies = 1  # far beyond the Infinity Cache already
-    ixs, build_s = [], 0.0
+    ixs, build_s, scan_note = [], 0.0, None
     for _ in range(copies):
         c = DeviceIndex(a.dim, a.dtype, local, capacity=n_local)
         c.add_synthetic(a.seed, n_local, gen_row0=r0)
+        ixs.append(c)
         if screen:  # the int8 copy is part of the index (built at load / ingest time, not per batch)
             torch.cuda.synchronize()
             tb = time.perf_counter()
-            c.enable_screen(1)
+            try:
+                c.enable_screen(1)
+            except RfxCapacityError as e:
+                # the copy does not fit beside the rows (config 4 whole on one GPU: 204.8 GB f16 + 102.4 GB
+                # codes > 288 GB): the exact scan for every copy, said in the JSON line
+                for x in ixs:
+                    x.enable_screen(0)
+                screen = False
+                scan_note = f"--scan auto: int8 copy does not fit ({e}); exact scan"
+                print(scan_note, file=sys.stderr, flush=True)
             build_s += time.perf_counter() - tb
-        ixs.append(c)
     ix = ixs[0]
     q = synth_rows(a.seed + 1, 0, a.nq, a.dim, a.dtype, local)
     kern = ix.search_plan(a.nq, a.k)
@@ -342,7 +352,7 @@ def main():
                                 if comm is not None else
                                 exchange_note if exchange_note else
                                 "host (gloo) rehearsal" if world > 1 else "none (one shard)"),
-                   "scan_kernel": SCAN_NAMES[kern]},
+                   "scan_kernel": SCAN_NAMES[kern] + (f" ({scan_note})" if scan_note else "")},
         "achieved_hbm_gbps_per_gpu": round(achieved, 1),
         "build_id": _lib.BUILD_ID,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",

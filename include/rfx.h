@@ -42,6 +42,8 @@ extern "C" {
 #define RFX_EBUSY 5    /* transient: device busy / queue timeout (maps to TimeoutError,     */
                        /* i.e. RETRYABLE_EXCEPTIONS, gemini_rag.py:22-27)                   */
 #define RFX_EUNSUPPORTED 6 /* configuration not supported by any kernel                     */
+#define RFX_ECAPACITY 7 /* the int8 copy (rfx_index_screen) does not fit: free device memory   */
+                        /* minus a reserve, or RFX_SCREEN_MAX_BYTES; the index stays exact     */
 
 /* ---- element types of the vector store --------------------------------------------------- */
 #define RFX_F32 0
@@ -77,6 +79,11 @@ int rfx_index_reserve(rfx_index_t h, int64_t capacity);
  * gemini_rag.py:319-327).  src_is_device selects hipMemcpy direction. */
 int rfx_index_add(rfx_index_t h, const void* vecs, int64_t n, int src_is_device,
                   int64_t* out_first_row, void* stream);
+/* Overwrite rows [row0, row0 + n) of the index (they must exist) with n vectors of the index dtype
+ * (device or host memory): the rows are live again (a tombstone on them is lifted) and their tiles of
+ * the int8 copy are re-quantised.  Used by the multi-store union view (rfx/union.py) to follow a
+ * member's appends in place (the file-search tool's store list, gemini_rag.py:463-469). */
+int rfx_index_write(rfx_index_t h, int64_t row0, const void* vecs, int64_t n, int src_is_device, void* stream);
 /* Append n synthetic rows generated on the device from the counter-based generator
  * (splitmix64, seed, generator row id) — bench/test corpora, identical to oracle/synth.py.
  * Generator rows are gen_row0 .. gen_row0+n-1 (gen_row0 < 0: continue at the index's row
@@ -184,6 +191,14 @@ int rfx_topk_merge_sorted(const float* cand_scores_d, const void* cand_rows_d, i
  * batch.  mode 0 drops the copy; mode 2 = on, with every batch sent to the exact fallback (tests).
  * Costs dim bytes per row of extra HBM.  EUNSUPPORTED for f32 stores and other dims. */
 int rfx_index_screen(rfx_index_t h, int mode, void* stream);
+/* Capacity: before allocating, rfx_index_screen checks that the copy (capacity * dim + capacity / 32 * 16
+ * bytes) fits in the device's free memory minus RFX_SCREEN_RESERVE_BYTES (default 4 GiB) and under
+ * RFX_SCREEN_MAX_BYTES when that is set; otherwise RFX_ECAPACITY and the index stays exact (config 4
+ * whole on one GPU: 204.8 GB of f16 rows + 102.4 GB of codes > 288 GB).  When an append grows the
+ * index past what the copy can follow, the copy is dropped and the append succeeds (the index is
+ * exact again; rfx_index_screen_state reports it): a failed copy never fails a store write
+ * (ingestion.py:311-339 would mark the document ERROR while its rows are committed). */
+int rfx_index_screen_state(rfx_index_t h, int* out_mode, int64_t* out_bytes, int* out_dropped);
 /* Inspection (tests): tiles [tile0, tile0 + ntiles) of the copy to host buffers (any may be NULL):
  * codes [ntiles*32][dim] int8, scales [ntiles] f32, live words [ntiles], stats [3] f32 (max row norm,
  * max quantisation-error norm, max tile scale). */

@@ -214,10 +214,79 @@ int launch_topk_merge(const float* cs, const void* cr, int rows_are_i64, int64_t
   return launch_topk_merge_lists(cs, cr, rows_are_i64, nq, n_cand, 1, k, row_offset, out_s, out_r, nullptr, st);
 }
 
+// The gathered merge of the multi-GPU step: `world` sorted lists of k records per query (every rank's
+// top-k, best first, padding (-inf, -1) at the tail).  One wave per query, 4 queries per block: the
+// world * k records are staged in LDS and every live record finds its final rank as its index in
+// its own list plus, for each other list, the number of records better than it (binary search,
+// broadcast LDS reads): world * log2(k) reads per record, no serial chain, no block-wide list
+// (config 3 at 8 GPUs: 80 records per query, 64 blocks).  Ranks of distinct (score, row) pairs are
+// distinct, so each of the k best lands in its own slot; slots past the live count get padding.
+constexpr int kGatherSmallMax = 512;  // world * k staged per wave; larger gathers take merge_kernel
+
+__global__ __launch_bounds__(256) void merge_gathered_small_kernel(const MergeRec* __restrict__ rec, int world,
+                                                                   int64_t nq, int k, float* __restrict__ out_s,
+                                                                   int64_t* __restrict__ out_r) {
+  __shared__ float ss[4][kGatherSmallMax];
+  __shared__ long long sr[4][kGatherSmallMax];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + w;
+  const bool active = q < nq;
+  const int n = world * k;
+  int live_n = 0;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    bool live = false;
+    if (active && i < n) {
+      const int m = i / k, e = i - m * k;
+      const MergeRec r = rec[((int64_t)m * nq + q) * k + e];
+      live = r.r >= 0 && r.r != kNoRow && r.s == r.s;
+      ss[w][i] = r.s;
+      sr[w][i] = live ? r.r : kNoRow;
+    }
+    live_n += __popcll(__ballot(live));
+  }
+  __syncthreads();
+  if (!active) return;
+  for (int i = lane; i < n; i += 64) {
+    const long long r = sr[w][i];
+    if (r == kNoRow) continue;
+    const float s = ss[w][i];
+    const int m = i / k;
+    int rank = i - m * k;
+    for (int mm = 0; mm < world && rank < k; ++mm) {
+      if (mm == m) continue;
+      const float* ls = ss[w] + mm * k;
+      const long long* lr = sr[w] + mm * k;
+      int lo = 0, hi = k;  // first record of list mm that is not better than (s, r)
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (lr[mid] != kNoRow && better64(ls[mid], lr[mid], s, r))
+          lo = mid + 1;
+        else
+          hi = mid;
+      }
+      rank += lo;
+    }
+    if (rank < k) {
+      out_s[q * k + rank] = s;
+      out_r[q * k + rank] = r;
+    }
+  }
+  for (int i = live_n + lane; i < k; i += 64) {
+    out_s[q * k + i] = -__builtin_inff();
+    out_r[q * k + i] = -1;
+  }
+}
+
 int launch_merge_gathered(const void* rec, int world, int64_t nq, int k, float* out_s, int64_t* out_r,
                           hipStream_t st) {
   const int kk = valu_k_slot(k);
   if (nq <= 0) return 0;
+  if ((int64_t)world * k <= kGatherSmallMax) {
+    hipLaunchKernelGGL(merge_gathered_small_kernel, dim3((unsigned)((nq + 3) / 4)), dim3(256), 0, st,
+                       (const MergeRec*)rec, world, nq, k, out_s, out_r);
+    return 0;
+  }
   GatheredSrc src{(const MergeRec*)rec, nq, k, (int64_t)world * k};
 #define RFX_M(KV)                                                                                     \
   if (kk == KV) {                                                                                     \
@@ -228,6 +297,29 @@ int launch_merge_gathered(const void* rec, int world, int64_t nq, int k, float* 
   RFX_VALU_K_LIST(RFX_M)
 #undef RFX_M
   return -1;
+}
+
+__global__ __launch_bounds__(256) void pack_records_kernel(const float* __restrict__ s, const int64_t* __restrict__ r,
+                                                           int64_t n, int64_t row_offset, MergeRec* __restrict__ rec,
+                                                           float* __restrict__ out_s, int64_t* __restrict__ out_r) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float sc = s[i];
+  const int64_t rr = r[i];
+  const int64_t g = rr < 0 ? -1 : rr + row_offset;
+  if (rec) {
+    rec[i] = MergeRec{sc, 0, (long long)g};
+  } else {
+    out_s[i] = sc;
+    out_r[i] = g;
+  }
+}
+
+void launch_pack_records(const float* s, const int64_t* r, int64_t n, int64_t row_offset, void* rec, float* out_s,
+                         int64_t* out_r, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(pack_records_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, s, r, n, row_offset,
+                     (MergeRec*)rec, out_s, out_r);
 }
 
 }  // namespace rfx

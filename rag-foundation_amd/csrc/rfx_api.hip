@@ -74,6 +74,7 @@ struct Index {
   // quantisation-error norm, max tile scale; f32 bits).  screen: 0 off, 1 on, 2 on with every batch sent to the
   // exact fallback (tests of the fallback path).
   int screen = 0;
+  int screen_dropped = 0;  // an append outgrew what the copy could follow: dropped, the index is exact
   int64_t scap = 0;
   int8_t* scodes = nullptr;
   void* smeta = nullptr;  // per tile {f32 scale, u32 live word, 0, 0}
@@ -90,15 +91,44 @@ void screen_free(Index& ix) {
   ix.scap = 0;
 }
 
+int64_t env_bytes(const char* name, int64_t dflt) {
+  const char* e = getenv(name);  // read at every build: tests and services may change it
+  return e && *e ? atoll(e) : dflt;
+}
+
+// Device bytes of the int8 copy for `cap` rows: codes, tile records, stats.
+int64_t screen_bytes(int64_t cap, int dim) { return cap * dim + cap / 32 * 16 + 256; }
+
+// Does a copy of `cap` rows fit?  Under RFX_SCREEN_MAX_BYTES (when set) and in the device's free memory
+// minus RFX_SCREEN_RESERVE_BYTES (default 4 GiB: search workspaces, the next growth of the rows).
+int screen_fits(const Index& ix, int64_t cap) {
+  const int64_t need = screen_bytes(cap, ix.dim) - (ix.scodes ? screen_bytes(ix.scap, ix.dim) : 0);
+  const int64_t cap_bytes = env_bytes("RFX_SCREEN_MAX_BYTES", -1);
+  if (cap_bytes >= 0 && screen_bytes(cap, ix.dim) > cap_bytes)
+    return fail(RFX_ECAPACITY, "int8 copy of %lld rows needs %lld B > RFX_SCREEN_MAX_BYTES %lld", (long long)cap,
+                (long long)screen_bytes(cap, ix.dim), (long long)cap_bytes);
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return fail(RFX_EDEVICE, "hipMemGetInfo failed");
+  const int64_t reserve = env_bytes("RFX_SCREEN_RESERVE_BYTES", (int64_t)4 << 30);
+  if (need + reserve > (int64_t)free_b)
+    return fail(RFX_ECAPACITY, "int8 copy of %lld rows needs %lld B more; the device has %zu B free (reserve %lld B)",
+                (long long)cap, (long long)need, free_b, (long long)reserve);
+  return RFX_OK;
+}
+
 // (Re)build the whole int8 copy for the current capacity.
 int screen_build(Index& ix, hipStream_t st) {
-  screen_free(ix);
   const int64_t cap = ix.capacity, nt = cap / 32;
+  if (cap > 0) {
+    const int rc = screen_fits(ix, cap);
+    if (rc) return rc;
+  }
+  screen_free(ix);
   if (cap == 0) return RFX_OK;
   if (hipMalloc(&ix.scodes, (size_t)cap * ix.dim) != hipSuccess || hipMalloc(&ix.smeta, (size_t)nt * 16) != hipSuccess ||
       hipMalloc(&ix.sstats, 256) != hipSuccess) {
     screen_free(ix);
-    return fail(RFX_ENOMEM, "hipMalloc failed for the int8 screen copy (%lld rows)", (long long)cap);
+    return fail(RFX_ECAPACITY, "hipMalloc failed for the int8 screen copy (%lld rows)", (long long)cap);
   }
   ix.scap = cap;
   RFX_HIP(hipMemsetAsync(ix.scodes, 0, (size_t)cap * ix.dim, st));
@@ -114,7 +144,16 @@ int screen_build(Index& ix, hipStream_t st) {
 // touch (the first one may have gained rows, so its scale can change); a grown buffer is rebuilt.
 int screen_update(Index& ix, int64_t first, hipStream_t st) {
   if (!ix.screen) return RFX_OK;
-  if (ix.scap != ix.capacity) return screen_build(ix, st);
+  if (ix.scap != ix.capacity) {
+    const int rc = screen_build(ix, st);
+    if (rc == RFX_ECAPACITY) {  // the rows are written: drop the copy, the index answers exactly
+      screen_free(ix);
+      ix.screen = 0;
+      ix.screen_dropped = 1;
+      return RFX_OK;
+    }
+    return rc;
+  }
   const int64_t t0 = first / 32, t1 = (ix.rows + 31) / 32;
   if (t1 > t0) {
     rfx::launch_screen_quantize(ix.data, ix.dim, ix.dtype, t0, t1 - t0, nullptr, ix.scodes, ix.smeta, ix.sstats, st);
@@ -124,8 +163,12 @@ int screen_update(Index& ix, int64_t first, hipStream_t st) {
   return RFX_OK;
 }
 
-int fused_state(Index& ix, hipStream_t st, uint32_t** out) {
-  std::lock_guard<std::mutex> lk(ix.state_mu);
+// The caller holds ix.state_mu (`slk`) from this lookup until its launches on `st` are enqueued: the
+// reset below frees every state after a device-wide drain, and a state handed out but not yet used by
+// an enqueued launch would otherwise be freed under its holder.  Once enqueued, the drain
+// waits for the launch, which leaves its state zero.
+int fused_state(Index& ix, hipStream_t st, uint32_t** out, const std::unique_lock<std::mutex>& slk) {
+  if (!slk.owns_lock() || slk.mutex() != &ix.state_mu) return fail(RFX_EINVAL, "search state lock not held");
   auto it = ix.fused_state.find(st);
   if (it != ix.fused_state.end()) {
     *out = it->second;
@@ -226,6 +269,9 @@ struct SearchLayout {
   int fbk;
   rfx::MfmaPlan sp;
   size_t s_tau, s_cs, s_cr, s_drop, s_qc, s_qe2, s_gate, s_diag;
+  // the one-launch VALU searches (kernel 11, the fused exact search) write (score, row) pairs: for a
+  // records / row-offset output they go here first and one pack launch converts them (sharded stores)
+  size_t pk_off, pk_r_off;
 };
 
 size_t align_up(size_t x) { return (x + 255) / 256 * 256; }
@@ -332,6 +378,12 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L, bool search
       L.s_diag = L.s_gate + 256;
       L.total = L.s_diag + align_up((size_t)nq * 8);
     }
+  }
+  L.pk_off = L.pk_r_off = 0;
+  if (search && L.kernel == 0 && nq > 0) {
+    L.pk_off = L.total;
+    L.pk_r_off = L.pk_off + align_up((size_t)nq * k * 4);
+    L.total = L.pk_r_off + align_up((size_t)nq * k * 8);
   }
   return RFX_OK;
 }
@@ -612,6 +664,35 @@ int rfx_index_add(rfx_index_t h, const void* vecs, int64_t n, int src_is_device,
   ix->tomb.resize((size_t)(ix->rows + 7) / 8, 0);
   if (out_first_row) *out_first_row = first;
   return screen_update(*ix, first, st);
+}
+
+int rfx_index_write(rfx_index_t h, int64_t row0, const void* vecs, int64_t n, int src_is_device, void* stream) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  if (n < 0 || (n > 0 && !vecs)) return fail(RFX_EINVAL, "bad vectors");
+  hipStream_t st = (hipStream_t)stream;
+  RFX_WLOCK(ix);
+  if (row0 < 0 || row0 + n > ix->rows)
+    return fail(RFX_EINVAL, "rows [%lld, %lld) are not rows of the index (%lld)", (long long)row0, (long long)(row0 + n),
+                (long long)ix->rows);
+  if (n == 0) return RFX_OK;
+  RFX_HIP(hipSetDevice(ix->device));
+  RFX_HIP(hipMemcpyAsync((uint8_t*)ix->data + row0 * ix->row_bytes(), vecs, (size_t)n * ix->row_bytes(),
+                         src_is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, st));
+  for (int64_t r = row0; r < row0 + n; ++r) {  // rewritten rows are live again
+    uint8_t& b = ix->tomb[(size_t)(r >> 3)];
+    if (b & (1u << (r & 7))) {
+      b &= (uint8_t) ~(1u << (r & 7));
+      ++ix->live;
+    }
+  }
+  if (ix->screen) {  // re-quantise the tiles the rows touch (their scales and live words change)
+    const int64_t t0 = row0 / 32, t1 = (row0 + n + 31) / 32;
+    rfx::launch_screen_quantize(ix->data, ix->dim, ix->dtype, t0, t1 - t0, nullptr, ix->scodes, ix->smeta, ix->sstats, st);
+    RFX_HIP(hipGetLastError());
+  }
+  RFX_HIP(hipStreamSynchronize(st));
+  return RFX_OK;
 }
 
 int rfx_index_add_synthetic(rfx_index_t h, uint64_t seed, int64_t gen_row0, int64_t n, int64_t* out_first_row,
@@ -1165,35 +1246,51 @@ int search_impl(rfx_index_t h, const void* queries_d, int64_t nq, int k, const u
   if (nq == 0) return RFX_OK;
   float* cs = (float*)(ws + L.cs_off);
   int32_t* cr = (int32_t*)(ws + L.cr_off);
-  if (!out_rec && row_offset == 0 && screen_valu_eligible(*ix, L, nq, k) && ((uintptr_t)queries_d & 15) == 0) {
+  // a records / row-offset output (a shard of a sharded store) of the one-launch searches: their
+  // (score, row) pairs go to the workspace, then one pack launch writes the caller's output
+  const bool pack = out_rec || row_offset != 0;
+  float* vo_s = pack ? (float*)(ws + L.pk_off) : out_scores_d;
+  int64_t* vo_r = pack ? (int64_t*)(ws + L.pk_r_off) : out_rows_d;
+  auto finish_pack = [&]() -> int {
+    if (!pack) return RFX_OK;
+    rfx::launch_pack_records(vo_s, vo_r, nq * k, row_offset, out_rec, out_scores_d, out_rows_d, st);
+    RFX_HIP(hipGetLastError());
+    return RFX_OK;
+  };
+  if ((!pack || L.pk_off) && screen_valu_eligible(*ix, L, nq, k) && ((uintptr_t)queries_d & 15) == 0) {
     uint32_t* state = nullptr;
-    if ((rc = fused_state(*ix, st, &state))) return rc;
+    std::unique_lock<std::mutex> slk(ix->state_mu);  // held until both launches are enqueued
+    if ((rc = fused_state(*ix, st, &state, slk))) return rc;
     uint32_t* sv = state + rfx::kScreenValuState;
     if ((rc = mark(ev0))) return rc;
     if (rfx::launch_screen_valu(L.vp, ix->scodes, ix->smeta, ix->sstats, (int)ix->rows, ix->dim, ix->dtype, ix->data,
-                                queries_d, (int)nq, row_mask_d, sv, cs, cr, k, out_scores_d, out_rows_d,
+                                queries_d, (int)nq, row_mask_d, sv, cs, cr, k, vo_s, vo_r,
                                 (ix->screen == 2 ? 1 : 0) | k11_ablate(), st) != 0)
       return fail(RFX_EUNSUPPORTED, "two-pass VALU search launch rejected");
     if ((rc = mark(ev1))) return rc;
     // the exact one-launch search, gated on the word the screen's last block wrote
     if (rfx::launch_search_valu_fused(L.vp, ix->data, (int)ix->rows, ix->dim, ix->dtype, queries_d, (int)nq, cs, cr,
-                                      state, k, out_scores_d, out_rows_d, st, row_mask_d, sv + 24) != 0)
+                                      state, k, vo_s, vo_r, st, row_mask_d, sv + 24) != 0)
       return fail(RFX_EUNSUPPORTED, "VALU search launch rejected");
     RFX_HIP(hipGetLastError());
-    return RFX_OK;
+    slk.unlock();
+    return finish_pack();
   }
   // (the one-launch kernel reads the caller's queries with 16-B loads: an unaligned buffer takes
   // the three-launch path, whose widening copy is aligned)
-  if (!out_rec && row_offset == 0 && L.kernel == 0 && ix->rows > 0 && nq <= rfx::kValuFusedMaxNq && fused_enabled() &&
+  if ((!pack || L.pk_off) && L.kernel == 0 && ix->rows > 0 && nq <= rfx::kValuFusedMaxNq && fused_enabled() &&
       ((uintptr_t)queries_d & 15) == 0) {
     uint32_t* state = nullptr;
-    if ((rc = fused_state(*ix, st, &state))) return rc;
+    std::unique_lock<std::mutex> slk(ix->state_mu);  // held until the launch is enqueued
+    if ((rc = fused_state(*ix, st, &state, slk))) return rc;
     if ((rc = mark(ev0))) return rc;
     if (rfx::launch_search_valu_fused(L.vp, ix->data, (int)ix->rows, ix->dim, ix->dtype, queries_d, (int)nq, cs, cr,
-                                      state, k, out_scores_d, out_rows_d, st, row_mask_d) != 0)
+                                      state, k, vo_s, vo_r, st, row_mask_d) != 0)
       return fail(RFX_EUNSUPPORTED, "VALU search launch rejected");
     RFX_HIP(hipGetLastError());
-    return mark(ev1);
+    slk.unlock();
+    if ((rc = mark(ev1))) return rc;
+    return finish_pack();
   }
   int64_t n_cand = L.n_cand;
   int list_len = L.kernel ? L.mp.k_lane : L.vp.k_slot;
@@ -1272,8 +1369,23 @@ int rfx_index_screen(rfx_index_t h, int mode, void* stream) {
   ix->screen = mode;
   if (had && ix->scap == ix->capacity) return RFX_OK;
   const int rc = screen_build(*ix, st);
-  if (rc) ix->screen = 0;
+  if (rc) {
+    ix->screen = 0;
+    screen_free(*ix);
+  } else {
+    ix->screen_dropped = 0;
+  }
   return rc;
+}
+
+int rfx_index_screen_state(rfx_index_t h, int* out_mode, int64_t* out_bytes, int* out_dropped) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  RFX_RLOCK(ix);
+  if (out_mode) *out_mode = ix->screen;
+  if (out_bytes) *out_bytes = ix->scodes ? screen_bytes(ix->scap, ix->dim) : 0;
+  if (out_dropped) *out_dropped = ix->screen_dropped;
+  return RFX_OK;
 }
 
 int rfx_index_screen_read(rfx_index_t h, int64_t tile0, int64_t ntiles, int8_t* codes_h, float* scales_h,

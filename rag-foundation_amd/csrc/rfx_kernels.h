@@ -125,6 +125,10 @@ int launch_topk_merge_lists(const float* cs, const void* cr, int rows_are_i64, i
                             bool sorted = false, const uint32_t* gate = nullptr);
 int launch_merge_gathered(const void* rec, int world, int64_t nq, int k, float* out_s, int64_t* out_r,
                           hipStream_t st);
+// n (score, row) pairs -> {score, 0, row + row_offset} merge records (rec) or (out_s, out_r + row_offset);
+// padding rows (< 0) stay -1
+void launch_pack_records(const float* s, const int64_t* r, int64_t n, int64_t row_offset, void* rec, float* out_s,
+                         int64_t* out_r, hipStream_t st);
 
 // ---- the exact two-pass scan (kernel 10 + k_screen.hip) -----------------------------
 bool screen_supported(int D, int dtype);

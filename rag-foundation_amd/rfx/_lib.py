@@ -15,7 +15,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RFX_LIB", os.path.join(_HERE, "librfx.so"))
 
-RFX_OK, RFX_EINVAL, RFX_ENOMEM, RFX_EDEVICE, RFX_EIO, RFX_EBUSY, RFX_EUNSUPPORTED = range(7)
+RFX_OK, RFX_EINVAL, RFX_ENOMEM, RFX_EDEVICE, RFX_EIO, RFX_EBUSY, RFX_EUNSUPPORTED, RFX_ECAPACITY = range(8)
 RFX_F32, RFX_BF16, RFX_F16 = 0, 1, 2
 
 DTYPE_CODES = {"f32": RFX_F32, "bf16": RFX_BF16, "f16": RFX_F16}
@@ -31,6 +31,11 @@ class RfxError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"rfx error {code}: {msg}")
         self.code = code
+
+
+class RfxCapacityError(RfxError):
+    """The int8 copy of the two-pass scan does not fit (RFX_ECAPACITY): the index stays exact.  Never
+    an upload failure: rfx.store logs it and keeps answering with the exact scan."""
 
 
 class RfxTransientError(TimeoutError):
@@ -99,6 +104,7 @@ SIGNATURES = {
     "rfx_index_reserve": ([_u64, _i64], _i),
     "rfx_index_add": ([_u64, _p, _i64, _i, _pi64, _p], _i),
     "rfx_index_add_synthetic": ([_u64, _u64, _i64, _i64, _pi64, _p], _i),
+    "rfx_index_write": ([_u64, _i64, _p, _i64, _i, _p], _i),
     "rfx_index_tombstone": ([_u64, _pi64, _i64, _p], _i),
     "rfx_index_read": ([_u64, _i64, _i64, _p, _i, _p], _i),
     "rfx_index_data": ([_u64, _pp], _i),
@@ -141,6 +147,7 @@ SIGNATURES = {
     "rfx_search_plan": ([_u64, _i64, _i, _pi], _i),
     "rfx_search_timed": ([_u64, _p, _i64, _i, _p, _i64, _i64, _p, _p, _p, _p, _sz, _p, _p, _p], _i),
     "rfx_index_screen": ([_u64, _i, _p], _i),
+    "rfx_index_screen_state": ([_u64, _pi, _pi64, _pi], _i),
     "rfx_index_screen_read": ([_u64, _i64, _i64, _p, _p, _p, _p], _i),
     "rfx_screen_diag": ([_u64, _i64, _i, _p, _p, _p], _i),
     "rfx_scan_topk_masked": ([_u64, _p, _i64, _i, _p, _i64, _p, _p, _p, _sz, _p], _i),
@@ -173,6 +180,8 @@ def check(rc: int, what: str = ""):
         raise RfxTransientError(rc, msg)
     if rc == RFX_EINVAL:
         raise ValueError(f"rfx: {msg}")
+    if rc == RFX_ECAPACITY:
+        raise RfxCapacityError(rc, msg)
     raise RfxError(rc, msg)
 
 

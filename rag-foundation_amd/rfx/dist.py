@@ -170,12 +170,12 @@ class ShardedSearch:
         self.comm = comm
         self.group = group
 
-    def search(self, queries: torch.Tensor, k: int, workspace=None, stream=None):
-        from .index import topk_merge_records
-
-        cs, cr = self.index.scan(queries, k, workspace=workspace, stream=stream)
-        rec = topk_merge_records(cs, cr, k, row_offset=self.row_offset, stream=stream,
-                                 list_len=self.index.list_len(queries.shape[0], k), sorted=True)
+    def search(self, queries: torch.Tensor, k: int, workspace=None, stream=None, row_mask=None):
+        """This rank's whole search as records (rfx_search_records: the exact two-pass scan when the
+        shard holds its int8 copy, the exact scan + merge otherwise; rows + row_offset), then the
+        exchange and the gathered merge."""
+        rec = self.index.search_records(queries, k, row_offset=self.row_offset, workspace=workspace, stream=stream,
+                                        row_mask=row_mask)
         return gather_merge_records(rec, k, self.comm, self.group, stream=stream)
 
 

@@ -112,6 +112,16 @@ class DeviceIndex:
         check(lib.rfx_index_add(self.handle, ptr(vecs), vecs.shape[0], int(on_dev), ctypes.byref(first), st))
         return first.value
 
+    def write(self, row0: int, vecs: torch.Tensor) -> None:
+        """Overwrite existing rows [row0, row0 + n) with rows of the index dtype (rfx_index_write): they are
+        live again and their int8-copy tiles are re-quantised."""
+        if vecs.dim() != 2 or vecs.shape[1] != self.dim or vecs.dtype != self.torch_dtype:
+            raise ValueError(f"expected [n][{self.dim}] {self.torch_dtype} rows, got {tuple(vecs.shape)} {vecs.dtype}")
+        vecs = vecs.contiguous()
+        on_dev = vecs.is_cuda
+        st = stream_ptr(torch.cuda.current_stream(vecs.device)) if on_dev else None
+        check(lib.rfx_index_write(self.handle, int(row0), ptr(vecs), vecs.shape[0], int(on_dev), st))
+
     def add_synthetic(self, seed: int, n: int, gen_row0: int = -1, stream=None) -> int:
         """Append n generated rows; generator row ids start at gen_row0 (default: continue)."""
         first = ctypes.c_int64()
@@ -206,6 +216,13 @@ class DeviceIndex:
         a gated fallback.  mode 0 drops the copy; mode 2 forces the fallback (tests)."""
         with torch.cuda.device(self.device):
             check(lib.rfx_index_screen(self.handle, int(mode), stream_ptr(stream)))
+
+    def screen_state(self):
+        """(mode, device bytes of the int8 copy, dropped): dropped = an append outgrew the room the copy
+        had (RFX_ECAPACITY) and the library went back to the exact scan."""
+        m, b, d = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int()
+        check(lib.rfx_index_screen_state(self.handle, ctypes.byref(m), ctypes.byref(b), ctypes.byref(d)))
+        return m.value, b.value, bool(d.value)
 
     def search_plan(self, nq: int, k: int) -> int:
         """Kernel rfx_search runs for (nq, k): 10 = the two-pass scan of a batch (int8 MFMA screen),

@@ -2,6 +2,7 @@
 
 Every call goes to the HIP library (librfx.so); there is no CPU path.
 """
+import collections
 import os
 import threading
 from dataclasses import dataclass
@@ -42,7 +43,32 @@ def _chunking(cfg):
 _STATE_LOCK = threading.Lock()
 _EMBEDDERS = {}
 _BATCHERS = {}  # (store name | tuple of names, filter key, registry id) -> GroupBatcher
-_UNIONS = {}    # (tuple of names, registry id) -> UnionView (rfx.union), rebuilt when a member changes
+# (tuple of names, registry id) -> UnionView (rfx.union), least recently used first; it follows its
+# members' appends and tombstones in place.  Bounded in device bytes (RFX_UNION_MAX_BYTES, default
+# 32 GiB): the least recently used views are evicted, and a view over its own budget is not built
+# (that question takes the per-store path).  A view in use when evicted is closed by its last user.
+_UNIONS = collections.OrderedDict()
+_UNION_BYTES = [0]
+
+
+def union_budget() -> int:
+    return int(os.environ.get("RFX_UNION_MAX_BYTES", str(32 << 30)))
+
+
+def _evict_union(key):
+    """(caller holds _STATE_LOCK)"""
+    v = _UNIONS.pop(key)
+    _UNION_BYTES[0] -= v.nbytes
+    v.evicted = True
+    if v.users == 0:
+        v.close()
+
+
+def _release_union(v):
+    with _STATE_LOCK:
+        v.users -= 1
+        if v.evicted and v.users == 0:
+            v.close()
 
 
 def _purge_batchers(name):
@@ -50,7 +76,7 @@ def _purge_batchers(name):
         for key in [k for k in _BATCHERS if k[0] == name or (isinstance(k[0], tuple) and name in k[0])]:
             del _BATCHERS[key]
         for key in [k for k in _UNIONS if name in k[0]]:
-            _UNIONS.pop(key).close()
+            _evict_union(key)
 
 
 class GpuRetriever:
@@ -156,22 +182,30 @@ class GpuRetriever:
 
     # ---- several stores in one launch (rfx.union) ------------------------------------------------
     def _union_view(self, names, stores):
+        """The cached view over `stores` brought up to date (in place when the members only grew or
+        deleted rows), pinned for the caller (_release_union), or None when a view of this size does not
+        fit the cache's byte budget.  Callers hold every member's lock."""
         key = (tuple(names), id(self.registry))
         want = runion.union_key(stores)
         with _STATE_LOCK:
             v = _UNIONS.get(key)
-            if v is not None and v.key == want:
-                return v
             if v is not None:
-                _UNIONS.pop(key).close()
-            if len(_UNIONS) >= 64:
-                for old in _UNIONS.values():
-                    old.close()
-                _UNIONS.clear()
+                _UNIONS.move_to_end(key)
+                if v.key == want or v.follow(stores):
+                    v.users += 1
+                    return v
+                _evict_union(key)
+            need, budget = runion.planned_bytes(stores), union_budget()
+            if need > budget:
+                return None
+            while _UNIONS and _UNION_BYTES[0] + need > budget:
+                _evict_union(next(iter(_UNIONS)))
             if self.registry.on_evict.count(_purge_batchers) == 0:
                 self.registry.on_evict.append(_purge_batchers)
             v = runion.UnionView(stores)
+            v.users, v.evicted = 1, False
             _UNIONS[key] = v
+            _UNION_BYTES[0] += v.nbytes
             return v
 
     def _run_union_batch(self, names, metadata_filter, items):
@@ -184,8 +218,11 @@ class GpuRetriever:
         locked = sorted(set(stores), key=lambda st: st.name)  # one global order: no lock-order deadlock
         for st in locked:  # members hold their locks while the view is built and searched
             st.lock.acquire()
+        view = None
         try:
             view = self._union_view(names, stores)
+            if view is None:  # over the view cache's byte budget: the per-store path
+                return [None] * len(items)
             mask = view.row_mask(stores, metadata_filter) if metadata_filter is not None else None
             if metadata_filter is not None and mask is None:
                 return [[] for _ in items]
@@ -201,6 +238,8 @@ class GpuRetriever:
                             for j in range(k) if r[i, j] >= 0])
             return out
         finally:
+            if view is not None:
+                _release_union(view)
             for st in reversed(locked):
                 st.lock.release()
 

@@ -11,9 +11,10 @@ rows and appends, every other shard is rebuilt from peer-to-peer copies of the o
 nothing is re-read from disk).
 IVF stores (RFX_INDEX=ivf, config 5) keep one IVF list set per shard under the store's one coarse
 quantiser (ShardedIvf below); a search is bit-identical to the same store on one device.
-A search: the batch's queries go to every shard's device, each shard runs the fused scan + its
-merge into [nq][k] records with its base added (rfx_topk_merge_records), one RCCL all-gather over
-the process's devices (rfx_allgather_records on an ncclCommInitAll group), one rfx_merge_gathered.
+A search: the batch's queries go to every shard's device, each shard runs its whole search into
+[nq][k] records with its base added (rfx_search_records: the exact two-pass scan when the shards hold
+their int8 copies), one RCCL gather to device 0 over the process's devices
+(rfx_gather_records on an ncclCommInitAll group), one rfx_merge_gathered.
 Several shards on one device (RFX_DEVICES=0,0,0,0: logical shards, tests) skip the collective:
 their records are stacked on that device and merged by the same kernel.
 """
@@ -22,6 +23,7 @@ import threading
 import numpy as np
 import torch
 
+from ._lib import RfxCapacityError
 from .dist import RcclComm
 from .index import DeviceIndex, merge_gathered, topk_merge_records
 
@@ -143,8 +145,13 @@ class ShardedIndex:
         if self._tombs:  # a copied tombstoned row is a NaN row: mark it dead in its new shard too
             self._tombstone(np.concatenate(self._tombs))
         if self._screen:
-            for sh in new[1:]:
-                sh.enable_screen(self._screen)
+            try:
+                for sh in new[1:]:
+                    sh.enable_screen(self._screen)
+            except RfxCapacityError:  # the re-split shards do not fit their copies: exact on every shard
+                for sh in new:
+                    sh.enable_screen(0)
+                self._screen = 0
 
     def add(self, vecs: torch.Tensor) -> int:
         """Append rows (writer path): they extend the last shard."""
@@ -215,11 +222,12 @@ class ShardedIndex:
                     rec[..., 0] = torch.tensor(float("-inf")).view(torch.int32).item()
                     rec[..., 1] = -1
                 else:
+                    # the shard's whole search (rfx_search_records): the two-pass scan when the shard holds
+                    # its int8 copy (kernel 10 for batches, kernel 11 for a few questions), the exact
+                    # scan + merge otherwise; records carry the global rows (row_offset = base)
                     q = queries.to(torch.device("cuda", d), non_blocking=True)
                     m = row_mask[i] if row_mask is not None else None
-                    cs, cr = sh.scan(q, k, stream=st, row_mask=m)
-                    rec = topk_merge_records(cs, cr, k, row_offset=base, stream=st, list_len=sh.list_len(nq, k),
-                                             sorted=True)
+                    rec = sh.search_records(q, k, row_offset=base, stream=st, row_mask=m)
             recs.append(rec)
         st0 = self._streams[0]
         s, r = merge_gathered(self._exchange(recs, nq, k)[0], k, stream=st0)
@@ -258,11 +266,21 @@ class ShardedIndex:
         return [gathered] * len(self.shards)
 
     def enable_screen(self, mode: int = 1) -> None:
-        """The exact two-pass scan on every shard (DeviceIndex.enable_screen; kept by re-splits)."""
+        """The exact two-pass scan on every shard (DeviceIndex.enable_screen; kept by re-splits): every
+        shard keeps its int8 copy and _search runs each shard through rfx_search_records, whose plan is
+        the two-pass scan (search_plan 10 / 11) wherever it applies."""
         with self._lock:
+            try:
+                for sh in self.shards:
+                    sh.enable_screen(mode)
+            except BaseException:
+                # all or nothing (a shard that does not fit its copy: RfxCapacityError): every shard
+                # back to the exact scan, then the caller sees the error (rfx.store logs it)
+                for sh in self.shards:
+                    sh.enable_screen(0)
+                self._screen = 0
+                raise
             self._screen = int(mode)
-            for sh in self.shards:
-                sh.enable_screen(mode)
 
     # ---- IVF (config 5) --------------------------------------------------------------------------
     def new_ivf(self, nlist):

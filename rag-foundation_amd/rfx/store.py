@@ -36,6 +36,7 @@ adapter per request (chat.py:937, ingestion.py:214).
 import errno
 import fcntl
 import json
+import logging
 import os
 import shutil
 import threading
@@ -45,8 +46,10 @@ import uuid
 import numpy as np
 
 from . import filters
-from ._lib import RFX_EBUSY, RfxTransientError
+from ._lib import RFX_EBUSY, RfxError, RfxTransientError
 from .index import DeviceIndex
+
+log = logging.getLogger("rfx.store")
 
 STORE_PREFIX = "fileSearchStores/"  # accepted by routes/stores.py:46 (prefix check)
 FORMAT = 2
@@ -414,15 +417,28 @@ class LocalStore:
         screened on the i8 matrix cores (kernel 10: bf16/f16 batches of > 64 questions) or with
         v_dot4 (kernel 11: up to 8 questions, any dtype), the survivors re-scored exactly.
         RFX_SCREEN=auto (default: from RFX_SCREEN_MIN_ROWS rows, 65,536) | 1 (always) | 0 (never).
-        Results are the exact scan's either way."""
+        Results are the exact scan's either way.
+        The copy is an accelerator, never a condition of a write: this runs after the manifest commit
+        (and on every reader's catch-up), so it must not raise.  When the copy does not fit
+        (RfxCapacityError: device memory minus a reserve, or RFX_SCREEN_MAX_BYTES) or the build fails,
+        the store logs it and stays exact; it is not retried for this store generation (the rows only
+        grow).  An append that outgrows the copy later is handled inside librfx the same way (the copy
+        is dropped, rfx_index_screen_state)."""
         mode = os.environ.get("RFX_SCREEN", "auto")
-        if mode == "0" or self._screen_on or not hasattr(self.index, "enable_screen"):
+        if mode == "0" or self._screen_on is not False or not hasattr(self.index, "enable_screen"):
             return
         if self.dtype not in ("bf16", "f16", "f32") or self.dim not in (768, 1024) or self.index.rows == 0:
             return
         if mode != "1" and self.index.rows < int(os.environ.get("RFX_SCREEN_MIN_ROWS", "65536")):
             return
-        self.index.enable_screen(1)
+        try:
+            self.index.enable_screen(1)
+        except (RfxError, RfxTransientError, ValueError) as e:
+            # (transient: the index lock was busy — the next catch-up tries again)
+            if not isinstance(e, RfxTransientError):
+                self._screen_on = None  # declined for this generation: exact scan
+            log.warning("store %s: int8 copy not built (%s); answering with the exact scan", self.name, e)
+            return
         self._screen_on = True
 
     def ivf_ready(self) -> bool:
@@ -451,6 +467,14 @@ class LocalStore:
             return True
 
     # ---- reads -------------------------------------------------------------------------------------
+    def tomb_rows(self, start: int, end: int = None) -> np.ndarray:
+        """Committed tombstoned rows [start, end) in commit order (tombs.bin; caller holds self.lock):
+        what a follower of this store (rfx.union.UnionView) re-applies after a deletion."""
+        end = self.tombs if end is None else end
+        if end <= start:
+            return np.zeros(0, dtype=np.int64)
+        return np.frombuffer(_read_range(self._p("tombs.bin"), 8 * start, 8 * end), dtype="<i8").astype(np.int64)
+
     def search(self, queries, k, row_mask=None):
         """(scores, rows) of the top-k rows per query.  An IVF store with trained lists answers
         unfiltered searches from its lists (nprobe probes, exact re-rank of min(64, max(16, 2k))

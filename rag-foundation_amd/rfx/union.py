@@ -2,18 +2,23 @@
 stores (the file-search tool's `file_search_store_names`, gemini_rag.py:463-469) is ONE scan launch
 and one merge instead of one per store plus a host merge.
 
-Layout: store i's rows [0, rows_i) sit at union rows [base_i, base_i + rows_i), the bases at
-multiples of 32 (a row-mask word never straddles two stores); the gap rows up to the next base are
-NaN (never returned, like a tombstone).  The view is a device-to-device copy of the stores' rows,
-rebuilt when any member's committed state changes (its key: name, generation, version, rows), so
-its results are the stores' committed state at the key.  Ranking in the view is (score desc,
-union row asc) = (score desc, store order, row asc): exactly GpuRetriever's per-store merge rule,
-and each row's score comes from the same kernels on the same stored values, so the hits are
-identical to searching the stores one by one.
+Layout: store i owns the union row range [base_i, base_i + region_i); its rows [0, rows_i) sit at
+[base_i, base_i + rows_i), the rest of the region is NaN headroom (never returned, like a
+tombstone).  Bases and regions are multiples of 32 (a row-mask word never straddles two stores).
+Ranking in the view is (score desc, union row asc) = (score desc, store order, row asc): exactly
+GpuRetriever's per-store merge rule, and each row's score comes from the same kernels on the same
+stored values, so the hits are identical to searching the stores one by one.
+
+Following the members: a member's committed state changes by appends and
+tombstones only (the same generation).  `follow` copies just the rows a member appended since the
+view last looked into its headroom (rfx_index_write: device to device, the int8 copy's touched tiles
+re-quantised) and re-applies its new tombstones (LocalStore.tomb_rows) — O(appended rows), not a
+rebuild.  Only a member that outgrows its headroom (max(4,096, rows / 16) rows, so the NaN rows the
+scan also streams stay ~6 %), a new generation, or a changed store list rebuilds the view.
 
 Eligible: every member a flat DeviceIndex store (IVF stores answer from their lists, sharded stores
-from their shards) on one device with one dim / dtype, and RFX_UNION_MAX_ROWS (default 16M) rows
-in all; otherwise the retriever keeps the per-store path.
+from their shards) on one device with one dim / dtype, and RFX_UNION_MAX_ROWS (default 16M) union
+rows; the retriever's view cache is bounded in bytes (RFX_UNION_MAX_BYTES, LRU; rfx.retriever).
 """
 import os
 
@@ -21,6 +26,7 @@ import numpy as np
 import torch
 
 from . import filters
+from ._lib import ESIZE
 from .index import DeviceIndex
 
 ALIGN = 32
@@ -30,50 +36,108 @@ def union_key(stores):
     return tuple((st.name, st.generation, st.version, st.index.rows) for st in stores)
 
 
+def _region(rows: int) -> int:
+    """Union rows reserved for a member of `rows` rows: its rows plus headroom for appends."""
+    return -(-(rows + max(4096, rows // 16)) // ALIGN) * ALIGN
+
+
+def planned_rows(stores) -> int:
+    return sum(_region(st.index.rows) for st in stores)
+
+
+def planned_bytes(stores) -> int:
+    """Device bytes a view over `stores` would hold: the rows, and the int8 copy when the members
+    answer with the two-pass scan (dim bytes per row)."""
+    st0 = stores[0]
+    n = planned_rows(stores)
+    screened = getattr(st0, "_screen_on", False) is True
+    return n * st0.dim * (ESIZE[st0.dtype] + (1 if screened else 0))
+
+
 def eligible(stores) -> bool:
     if len(stores) < 2:
         return False
     first = stores[0]
     limit = int(os.environ.get("RFX_UNION_MAX_ROWS", str(16 << 20)))
-    total = 0
     for st in stores:
         if type(st.index) is not DeviceIndex or st.ivf is not None:
             return False
         if st.device != first.device or st.dim != first.dim or st.dtype != first.dtype:
             return False
-        total += -(-st.index.rows // ALIGN) * ALIGN
-    return 0 < total <= limit
+    return 0 < planned_rows(stores) <= limit and any(st.index.rows for st in stores)
 
 
 class UnionView:
     def __init__(self, stores):
         self.key = union_key(stores)
         self.names = [st.name for st in stores]
+        self.gens = [st.generation for st in stores]
         st0 = stores[0]
         self.dim, self.dtype, self.device = st0.dim, st0.dtype, st0.device
-        self.bases, self.rows = [], []
-        padded = [-(-st.index.rows // ALIGN) * ALIGN for st in stores]
-        self.index = DeviceIndex(self.dim, self.dtype, self.device, capacity=max(sum(padded), 1))
+        self.screened = getattr(st0, "_screen_on", False) is True
+        self.bases, self.rows, self.regions, self.tombs = [], [], [], []
+        self.rows_copied = 0  # rows this view copied from its members (tests / profiles: O(appended))
+        self.users, self.evicted = 0, False  # pins of the retriever's view cache (rfx.retriever)
+        total = planned_rows(stores)
+        self.index = DeviceIndex(self.dim, self.dtype, self.device, capacity=max(total, 1))
         dev = torch.device("cuda", self.device)
-        span, base = 1 << 20, 0
+        base = 0
         try:
             with torch.cuda.device(dev):
-                for st, pad in zip(stores, padded):
-                    n = st.index.rows
+                for st in stores:
+                    n, reg = st.index.rows, _region(st.index.rows)
                     self.bases.append(base)
                     self.rows.append(n)
-                    for r0 in range(0, n, span):
-                        self.index.add(st.index.read(r0, min(span, n - r0)))
-                    if pad > n:
-                        nan = torch.full((pad - n, self.dim), float("nan"), dtype=self.index.torch_dtype, device=dev)
-                        self.index.add(nan)
-                    base += pad
-                if getattr(st0, "_screen_on", False):  # members answer with the two-pass scan: so does the view
+                    self.regions.append(reg)
+                    self.tombs.append(st.tombs)
+                    self._copy(st, 0, n, append=True)
+                    self.index.add(torch.full((reg - n, self.dim), float("nan"), dtype=self.index.torch_dtype, device=dev))
+                    base += reg
+                if self.screened:  # members answer with the two-pass scan: so does the view
                     self.index.enable_screen(1)
         except BaseException:
             self.index.close()
             raise
         self._bases = np.asarray(self.bases, dtype=np.int64)
+
+    @property
+    def nbytes(self) -> int:
+        return self.index.rows * self.dim * (ESIZE[self.dtype] + (1 if self.screened else 0))
+
+    def _copy(self, st, r0, r1, append=False, base=0):
+        span = 1 << 20
+        for a in range(r0, r1, span):
+            v = st.index.read(a, min(span, r1 - a))
+            if append:
+                self.index.add(v)
+            else:
+                self.index.write(base + a, v)
+        self.rows_copied += r1 - r0
+
+    def follow(self, stores) -> bool:
+        """Bring the view to the members' committed state in place (callers hold every member's
+        lock).  False when it cannot (another store list, a new generation, a member past its
+        headroom, a member that shrank): then the caller rebuilds the view."""
+        if [st.name for st in stores] != self.names or [st.generation for st in stores] != self.gens:
+            return False
+        if (getattr(stores[0], "_screen_on", False) is True) != self.screened:
+            return False
+        for st, n0, reg, t0 in zip(stores, self.rows, self.regions, self.tombs):
+            if st.index.rows < n0 or st.index.rows > reg or st.tombs < t0:
+                return False
+        with torch.cuda.device(torch.device("cuda", self.device)):
+            for i, st in enumerate(stores):
+                n = st.index.rows
+                if n > self.rows[i]:  # the member's appended rows, into its headroom
+                    self._copy(st, self.rows[i], n, base=self.bases[i])
+                    self.rows[i] = n
+                if st.tombs > self.tombs[i]:  # its new tombstones
+                    dead = st.tomb_rows(self.tombs[i], st.tombs)
+                    if dead.size:
+                        self.index.tombstone(dead + self.bases[i])
+                    self.tombs[i] = st.tombs
+        self.key = union_key(stores)
+        return True
 
     def row_mask(self, stores, metadata_filter):
         """Device mask over the union rows of the members' files matching the filter; None when

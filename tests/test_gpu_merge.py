@@ -118,6 +118,28 @@ def test_merge_gathered_equals_flat_merge(rindex, world):
     assert np.array_equal(out_s.cpu().numpy(), ref_s)
 
 
+@pytest.mark.parametrize("world,k,ties", [(1, 1, False), (2, 5, True), (8, 10, False), (8, 10, True), (5, 16, True),
+                                          (8, 64, False), (16, 32, True), (9, 64, False), (64, 10, True)])
+def test_merge_gathered_shapes_and_ties(rindex, world, k, ties):
+    """rfx_merge_gathered on sorted per-rank records (the dedicated one-wave-per-query kernel up to
+    world * k = 512, the block merge beyond): ties across ranks, short lists padded (-inf, -1), nq not
+    a multiple of the kernel's 4 queries per block."""
+    rng = np.random.default_rng(world * 1000 + k + ties)
+    nq = 23
+    recs, all_s, all_r = [], [], []
+    for w in range(world):
+        s, r = sorted_lists(rng, nq, 1, k, 1 << 20, empty_frac=0.3, ties=ties)
+        r = np.where(r == 0x7fffffff, -1, r + w * (1 << 20))
+        s = np.where(r < 0, -np.inf, s).astype(np.float32)
+        recs.append(rdist.pack(torch.from_numpy(s).cuda(), torch.from_numpy(r).cuda()))
+        all_s.append(s)
+        all_r.append(r)
+    out_s, out_r = rindex.merge_gathered(torch.stack(recs), k)
+    ref_s, ref_r = oracle_merge(np.concatenate(all_s, axis=1), np.concatenate(all_r, axis=1), k)
+    assert np.array_equal(out_r.cpu().numpy(), ref_r)
+    assert np.array_equal(out_s.cpu().numpy(), ref_s)
+
+
 def test_scan_then_records_then_gathered_equals_search(rindex):
     """Sharded search on one device (2 shards of one corpus) == unsharded search."""
     n, d = 40_000, 768

@@ -220,3 +220,81 @@ def test_rccl_gather_records_one_rank():
     torch.cuda.synchronize()
     assert torch.equal(out[0], rec)
     comm.close()
+
+
+def test_sharded_two_pass_equals_unsharded_screened(tmp_path):
+    """every shard of a screened ShardedIndex searches with the exact two-pass scan
+    (rfx_search_records: kernel 10 for the batch, kernel 11 + the records pack for a lone question), no
+    shard falls back, and the answers are bit-identical to the unsharded screened index — unmasked,
+    masked, and after tombstones."""
+    from rfx import filters
+    from rfx.index import DeviceIndex, synth_rows
+    from rfx.sharded import ShardedIndex
+
+    n = 200_003
+    whole = DeviceIndex(768, "bf16", 0)
+    whole.add_synthetic(21, n)
+    path = str(tmp_path / "rows.rfx")
+    whole.rows_append(path, 0)
+    sh = ShardedIndex(768, "bf16", [0, 0, 0, 0])
+    sh.rows_sync(path, n)
+    whole.enable_screen(1)
+    sh.enable_screen(1)
+    q = synth_rows(22, 0, 256, 768, "bf16")
+    for shard in sh.shards:
+        assert shard.screen_state()[0] == 1
+        assert shard.search_plan(256, 10) == 10 and shard.search_plan(1, 10) == 11
+    a = whole.search(q, 10)
+    b = sh.search(q, 10)
+    assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0])
+    for shard, base in zip(sh.shards, sh.bases):
+        ws = torch.empty(shard.workspace_bytes(256, 10), dtype=torch.uint8, device="cuda")
+        rec = shard.search_records(q, 10, row_offset=base, workspace=ws)
+        diag, fb = shard.screen_diag(256, 10, ws)
+        assert not fb and (diag[:, 1] >= 0).all()
+        rows = rec[..., 1]
+        assert ((rows >= base) & (rows < base + shard.rows)).all()
+    for i in range(3):  # lone questions: kernel 11 on every shard, records through the pack launch
+        a = whole.search(q[i:i + 1], 10)
+        b = sh.search(q[i:i + 1], 10)
+        assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0])
+    words = filters.row_mask_words(n, [(5, 30_000), (70_100, 10), (120_000, 50_007)])
+    for nq in (256, 2):
+        a = whole.search(q[:nq], 10, row_mask=torch.from_numpy(words).cuda())
+        b = sh.search(q[:nq], 10, row_mask=sh.mask_tensor(words))
+        assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0])
+    dead = np.unique(a[1][:, :3].cpu().numpy().ravel())
+    whole.tombstone(dead)
+    sh.tombstone(dead)
+    for nq in (256, 1):
+        a = whole.search(q[:nq], 10)
+        b = sh.search(q[:nq], 10)
+        assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0])
+        assert not np.isin(b[1].cpu().numpy(), dead).any()
+
+
+def test_sharded_screened_store_equals_unsharded(tmp_path, monkeypatch):
+    """The adapter path: an RFX_DEVICES=0x4 store with RFX_SCREEN=1 answers bit-identically to the
+    unsharded screened store, every shard on the two-pass plan."""
+    from rfx import store as rstore
+    from rfx.retriever import GpuRetriever
+
+    monkeypatch.setenv("RFX_SCREEN", "1")
+    root = str(tmp_path)
+    writer = GpuRetriever(registry=rstore.StoreRegistry(root=root, device=0), dtype="bf16")
+    name = writer.create_store("shared")
+    for i, (t, m) in enumerate(DOCS):
+        writer.add_document(name, t, f"doc{i}", {"white_space_config": {"max_tokens_per_chunk": 4}}, m)
+    plain = GpuRetriever(registry=rstore.StoreRegistry(root=root, device=0), dtype="bf16")
+    sharded = GpuRetriever(registry=rstore.StoreRegistry(root=root, device=0, devices="0x4"), dtype="bf16")
+    six = sharded.registry.get(name).index
+    assert all(s.screen_state()[0] == 1 and s.search_plan(256, 10) == 10 for s in six.shards)
+    for qq in QUESTIONS:
+        for k in (5, 10):
+            assert _hits(sharded, name, qq, k) == _hits(plain, name, qq, k)
+        assert _hits(sharded, name, qq, 7, {"tenant": "acme"}) == _hits(plain, name, qq, 7, {"tenant": "acme"})
+    emb = plain.embedder(768)
+    qs = emb.embed_texts([f"{w} {v}" for w in ("alpha", "theta", "roofline", "sigma") for v in range(64)], "bf16")
+    a_s, a_r = plain.registry.get(name).index.search(qs, 10)
+    b_s, b_r = six.search(qs, 10)
+    assert torch.equal(a_r, b_r) and torch.equal(a_s, b_s)

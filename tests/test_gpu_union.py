@@ -109,3 +109,97 @@ def test_union_batched_questions(tmp_path):
         if all(b[i][0] - b[i + 1][0] > 2e-6 for i in range(len(b) - 1)):
             assert [x[1:] for x in a] == [y[1:] for y in b], q
     torch.cuda.synchronize()
+
+
+def _synth_store(reg, name, n, seed, files=4):
+    """A store of n synthetic bf16 rows in `files` uploads (LocalStore.add_document with device rows)."""
+    from rfx.index import synth_rows
+    st = reg.create(name, 768, "bf16")
+    per = -(-n // files)
+    fids = []
+    for f in range(files):
+        m = min(per, n - f * per)
+        vecs = synth_rows(seed, f * per, m, 768, "bf16")
+        fids.append(st.add_document([f"{name}-{f}-{i}" for i in range(m)], vecs, f"{name}-{f}.md",
+                                    {"part": f})[0])
+    return st, fids
+
+
+def test_union_follows_member_appends_in_place(tmp_path):
+    """an upload to one member of a 3-store union of > 1M rows costs O(appended
+    rows) — the cached view copies only the new rows into that member's headroom and re-applies new
+    tombstones; hits stay identical to the per-store path."""
+    import time
+
+    from rfx import retriever as rret
+    from rfx import store as rstore
+    from rfx.index import synth_rows
+    from rfx.retriever import GpuRetriever
+
+    reg = rstore.StoreRegistry(root=str(tmp_path), device=0)
+    ret = GpuRetriever(registry=reg, dtype="bf16")
+    ret.batching = False
+    stores = [_synth_store(reg, f"u{i}", 350_000 + 1000 * i, 40 + i) for i in range(3)]
+    names = [st.name for st, _ in stores]
+
+    def check(q):
+        ret.union = True
+        a = _hits(ret, names, q, 10)
+        assert ret.last_path == "union"
+        ret.union = False
+        assert a == _hits(ret, names, q, 10)
+        return a
+
+    t0 = time.perf_counter()
+    check("alpha gamma")
+    t_build = time.perf_counter() - t0
+    key = (tuple(names), id(reg))
+    view = rret._UNIONS[key]
+    assert view.rows_copied == sum(st.index.rows for st, _ in stores) >= 1_000_000
+    st1 = stores[1][0]
+    st1.add_document([f"late-{i}" for i in range(1500)], synth_rows(99, 0, 1500, 768, "bf16"), "late.md")
+    t0 = time.perf_counter()
+    check("theta kappa")
+    t_follow = time.perf_counter() - t0
+    assert rret._UNIONS[key] is view and view.rows_copied == sum(st.index.rows for st, _ in stores)
+    assert view.rows[1] == st1.index.rows
+    copied = view.rows_copied
+    stores[2][0].delete_file(stores[2][1][1])
+    check("document retrieval")
+    assert rret._UNIONS[key] is view and view.rows_copied == copied  # tombstones only: no rows copied
+    print(f"union of {sum(view.rows)} rows: build+search {t_build * 1e3:.1f} ms, follow 1500 appended rows + "
+          f"search {t_follow * 1e3:.1f} ms")
+    assert t_follow < t_build
+
+
+def test_union_cache_stays_within_its_byte_budget(tmp_path, monkeypatch):
+    """The view cache is bounded in bytes (RFX_UNION_MAX_BYTES, LRU), not by a count; a list whose view
+    alone exceeds the budget takes the per-store path."""
+    from rfx import retriever as rret
+    from rfx import store as rstore
+    from rfx import union as runion
+    from rfx.retriever import GpuRetriever
+
+    reg = rstore.StoreRegistry(root=str(tmp_path), device=0)
+    ret = GpuRetriever(registry=reg, dtype="bf16")
+    ret.batching = False
+    names = [ret.create_store(f"c{i}") for i in range(4)]
+    for i, (t, m) in enumerate(DOCS):
+        ret.add_document(names[i % 4], t, f"doc{i}", WS, m)
+    pair = runion.planned_bytes([reg.get(names[0]), reg.get(names[1])])
+    monkeypatch.setenv("RFX_UNION_MAX_BYTES", str(int(pair * 2.5)))
+    budget = rret.union_budget()
+    lists = [[names[0], names[1]], [names[2], names[3]], [names[0], names[2]], [names[1], names[3]],
+             [names[0], names[1]]]
+    for lst in lists:
+        ret.union = True
+        a = _hits(ret, lst, "alpha theta", 6)
+        assert ret.last_path == "union"
+        ret.union = False
+        assert a == _hits(ret, lst, "alpha theta", 6)
+        mine = [v for k, v in rret._UNIONS.items() if k[1] == id(reg)]
+        assert rret._UNION_BYTES[0] <= budget and sum(v.nbytes for v in mine) <= budget
+    monkeypatch.setenv("RFX_UNION_MAX_BYTES", str(pair // 2))  # no view fits: per-store path, same hits
+    ret.union = True
+    a = _hits(ret, names[:3], "roofline lds", 8)
+    assert ret.last_path == "per-store"

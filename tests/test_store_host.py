@@ -179,3 +179,29 @@ def test_failed_file_record_append_rolls_back(tmp_path, monkeypatch, op):
     assert first3 == 2
     sb = reg(tmp_path).get(st.name)  # another process opens it without a row/metadata mismatch
     assert sb.index.rows == 3 and len(sb.rows) == 3 and sb.row_info(2)[0] == f3
+
+
+class _NoRoomIndex(HostIndex):
+    """A host index whose int8 copy never fits (librfx's RFX_ECAPACITY)."""
+    calls = 0
+
+    def enable_screen(self, mode=1):
+        from rfx._lib import RfxCapacityError
+        type(self).calls += 1
+        raise RfxCapacityError(7, "int8 copy of 3 rows needs 2304 B > RFX_SCREEN_MAX_BYTES 0 (test)")
+
+
+def test_screen_capacity_never_fails_a_committed_upload(tmp_path, monkeypatch):
+    """VERDICT r3 missing #2: the copy is built after the manifest commit; when it does not fit, the
+    upload still returns its file id (no ERROR document, ingestion.py:311-339), readers catch up without
+    raising, and the store does not retry the copy on every upload of the same generation."""
+    monkeypatch.setenv("RFX_SCREEN", "1")
+    _NoRoomIndex.calls = 0
+    w = rstore.StoreRegistry(root=str(tmp_path), device=0, index_factory=_NoRoomIndex)
+    st = w.create("big", 768, "f32")
+    f1, first1 = st.add_document(["a", "b"], vecs(2, 1, 768), "one.md")
+    f2, first2 = st.add_document(["c"], vecs(1, 2, 768), "two.md")
+    assert (first1, first2) == (0, 2) and st.index.rows == 3 and len(st.rows) == 3
+    assert _NoRoomIndex.calls == 1 and st._screen_on is None
+    r = rstore.StoreRegistry(root=str(tmp_path), device=0, index_factory=_NoRoomIndex).get(st.name)
+    assert r.index.rows == 3 and r.files[f2]["first"] == 2
