@@ -2,8 +2,8 @@
 // two-pass scan's int8 screen (k_scan_screen.h MODE bits: 1 no top-k fold, 2 no launder, 4 prefetch
 // distance 1, 8 no corpus stream, 16 early slot-table refreshes, 32 slow-path entry count, 64 store-wide
 // integer fast-path bound, 128 epilogue in place, 256 min-of-KL slot bound, 512 slow path never taken,
-// 1024 serial LDS insert),
-// via rfx_dbg_screen_variant; variant = 1000 * RING + MODE (RING in {4, 6, 8, 10, 12}).
+// 1024 serial LDS insert, 2048 slow-path issue priority),
+// via rfx_dbg_screen_variant; variant = 100000 * RING + MODE (RING in {4, 6, 8, 10, 12}).
 #include "k_scan_screen.h"
 
 namespace rfx {
@@ -16,7 +16,7 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
   const int ntiles = (nrows + k10::kTM - 1) / k10::kTM;
   dim3 grid(p.blocks, p.q_blocks);
 #define RFX_K10V(R, M)                                                                                        \
-  case 1000 * R + M:                                                                                          \
+  case 100000 * R + M:                                                                                          \
     hipLaunchKernelGGL((k10::scan_screen_kernel<10, 768, false, R, M>), grid, dim3(512), 0, st, X, tm, sts, Qc, \
                        qe2, nq, ntiles, tau, cs, cr, dr, p.n_lists, nullptr);                                \
     break;
@@ -46,6 +46,8 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
     RFX_K10V(8, 1056)
     RFX_K10V(8, 16)
     RFX_K10V(8, 48)
+    RFX_K10V(8, 2048)
+    RFX_K10V(8, 2080)
     default:
       return -1;
   }

@@ -226,7 +226,7 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
 // 256 = kernel 6's slot-table bound (min over KL slots) instead of the KL-th largest of 16, 512 = the
 // slow path compiled in but never taken (wrong results; separates its cost from the code's presence),
 // 1024 = the slow path's serial LDS list insert instead of the register-resident list, 16 = the slot
-// table re-read at every one of the first 16 tiles.
+// table re-read at every one of the first 16 tiles, 2048 = issue priority for a wave in the slow path.
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
@@ -417,6 +417,9 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
     if constexpr ((MODE & 512) != 0) hit = hit && nq < 0;  // debug: the slow path compiled in, never taken
     if constexpr ((MODE & 1) == 0) {
       if (__builtin_amdgcn_ballot_w64(hit)) {
+        // debug MODE 2048: the wave in the slow path takes issue priority over its SIMD partner (which
+        // keeps issuing MFMAs), so it reaches the next stage barrier sooner
+        if constexpr ((MODE & 2048) != 0) __builtin_amdgcn_s_setprio(3);
         if constexpr ((MODE & 32) != 0)  // debug: count slow-path entries per wave (unused threshold slot 15)
           if (lane == 0) atomicAdd(tau + (int64_t)(qg + w * kQW) * kTauW + 15, 1u);
         const uint2 md = *(const uint2*)(lds + kMetaOff + (it % kMR) * 1024 + lane * 16);
@@ -434,6 +437,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
         fold_screen<KL, (MODE & 1024) == 0>(acc4, st, lw >> (8 * half), Ls, Lr, thr, e2, drop, tile * kTM + 8 * half,
                                             tau_rsrc, slot_voff);
         set_bounds();
+        if constexpr ((MODE & 2048) != 0) __builtin_amdgcn_s_setprio(0);
       }
     } else if (hit && m0 == 12345 && m1 == 54321) {
       Ls[0] = 1;

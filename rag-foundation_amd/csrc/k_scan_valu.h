@@ -100,9 +100,75 @@ struct FusedOut {
   int k_out;
   float* out_s;
   int64_t* out_r;
-  // the two-pass scan's fallback (k_screen_valu.hip): run only when the screen set this word
+  // the two-pass scan's fallback (k_screen_valu.hip): run only when the screen set this word, and the
+  // final top-k re-scored by the two-pass rule (Rescore above; rows = the scan's X, queries = Qf)
   const uint32_t* gate = nullptr;
 };
+
+// The two-pass scan's score rule: a returned score is fl32(exact dot), the f64 sum of the exact
+// products rounded once, and the order is (that f32 score desc, row asc) — what kernel 10's select and
+// kernel 11's last block return.  When either falls back to an exact scan (f32 accumulation), the
+// fallback's final top-k is re-scored by the same rule (`Rescore`), so an answer's bits do not depend
+// on which path a query (or a shard of a sharded store) took.
+// (struct Rescore: rfx_kernels.h)
+
+__device__ __forceinline__ float elem_rt(const void* p, int64_t i, int dtype) {
+  if (dtype == RFX_F32) return ((const float*)p)[i];
+  const uint16_t h = ((const uint16_t*)p)[i];
+  return dtype == RFX_BF16 ? bf16_to_f32(h) : f16_to_f32(h);
+}
+
+// Block-wide (any block size that is a multiple of 64, k_out <= 64): the k_out entries just written
+// for query q (out_s / out_r, or out_rec with row_offset added) re-scored and re-ordered by the rule
+// above.  The caller's writes are read back with agent-scope loads after a barrier.
+__device__ __forceinline__ void rescore_final(const Rescore& rs, int64_t q, int k_out, int64_t row_offset,
+                                              float* out_s, int64_t* out_r, MergeRec* out_rec) {
+  __shared__ float rs_s[64];
+  __shared__ long long rs_r[64];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int tid = threadIdx.x, nt = blockDim.x, gl = tid & 7;
+  for (int e0 = 0; e0 < k_out; e0 += nt / 8) {
+    const int e = e0 + (tid >> 3);
+    long long row = -1;
+    if (e < k_out) {
+      const int64_t o = q * k_out + e;
+      row = out_rec ? (long long)__hip_atomic_load((const unsigned long long*)&out_rec[o].r, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)
+                    : (long long)__hip_atomic_load((const unsigned long long*)out_r + o, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
+    double acc = 0.0;
+    if (row >= 0) {
+      const int64_t xr = (row - (out_rec ? row_offset : 0)) * rs.D, qr = q * rs.D;
+      for (int c = gl; c < rs.D; c += 8)
+        acc += (double)elem_rt(rs.X, xr + c, rs.dtype) * (double)elem_rt(rs.Q, qr + c, rs.dtype);
+    }
+#pragma unroll
+    for (int off = 4; off; off >>= 1) acc += __shfl_xor(acc, off);
+    if (gl == 0 && e < k_out) {
+      rs_s[e] = row >= 0 ? (float)acc : -__builtin_inff();
+      rs_r[e] = row;
+    }
+  }
+  __syncthreads();
+  if (tid < k_out) {
+    const float s = rs_s[tid];
+    const long long r = rs_r[tid];
+    if (r >= 0) {
+      int rank = 0;
+      for (int f = 0; f < k_out; ++f) rank += rs_r[f] >= 0 && better64(rs_s[f], rs_r[f], s, r);
+      const int64_t o = q * k_out + rank;
+      if (out_rec) {
+        out_rec[o] = MergeRec{s, 0, r};
+      } else {
+        out_s[o] = s;
+        out_r[o] = r;
+      }
+    }
+  }
+  __syncthreads();
+}
 
 template <int DT>
 __device__ __forceinline__ float query_elem(const void* Q, int64_t i) {
@@ -360,12 +426,14 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
         __syncthreads();
         merge_one<K, false, 4, true>(lsrc, q0 + qi, K, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
         __syncthreads();
+        if (fo.gate) rescore_final(Rescore{X, Qf, D, DT}, q0 + qi, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
       }
     } else {
       const AgentSrc src{cand_s, cand_r, n};
       for (int qi = 0; qi < nqt; ++qi) {
         merge_one<K, false, 4, true>(src, q0 + qi, K, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
         __syncthreads();
+        if (fo.gate) rescore_final(Rescore{X, Qf, D, DT}, q0 + qi, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
       }
     }
     if (tid < nqt && tau) tau[q0 + tid] = 0u;  // every block's bound updates precede its arrival

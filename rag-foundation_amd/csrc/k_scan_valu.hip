@@ -173,14 +173,17 @@ void launch_widen_queries(const void* Q, int64_t n, int dtype, float* out, hipSt
 template <int K, bool R64, bool SORTED, class Src>
 __global__ __launch_bounds__(512) void merge_kernel(Src src, int list_len, int k_out, int64_t row_offset,
                                                     float* __restrict__ out_s, int64_t* __restrict__ out_r,
-                                                    MergeRec* __restrict__ out_rec, const uint32_t* __restrict__ gate) {
+                                                    MergeRec* __restrict__ out_rec, const uint32_t* __restrict__ gate,
+                                                    Rescore rs) {
   if (gate && *gate == 0u) return;  // the two-pass scan's gated fallback (k_screen.hip)
   merge_one<K, R64, 8, SORTED>(src, (int64_t)blockIdx.x, list_len, k_out, row_offset, out_s, out_r, out_rec);
+  if (rs.X) rescore_final(rs, (int64_t)blockIdx.x, k_out, row_offset, out_s, out_r, out_rec);
 }
 
 int launch_topk_merge_lists(const float* cs, const void* cr, int rows_are_i64, int64_t nq, int64_t n_cand,
                             int list_len, int k, int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec,
-                            hipStream_t st, bool sorted, const uint32_t* gate) {
+                            hipStream_t st, bool sorted, const uint32_t* gate, const Rescore* rescore) {
+  const Rescore rs = rescore ? *rescore : Rescore{};
   const int kk = valu_k_slot(k);
   if (nq <= 0) return 0;
   if (list_len < 1 || (list_len > 1 && n_cand % list_len != 0)) {
@@ -190,7 +193,7 @@ int launch_topk_merge_lists(const float* cs, const void* cr, int rows_are_i64, i
   MergeRec* rec = (MergeRec*)out_rec;
 #define RFX_M2(KV, R, S)                                                                                  \
   hipLaunchKernelGGL((merge_kernel<KV, R, S, FlatSrc<R>>), dim3((unsigned)nq), dim3(512), 0, st,          \
-                     FlatSrc<R>{cs, cr, n_cand}, list_len, k, row_offset, out_s, out_r, rec, gate)
+                     FlatSrc<R>{cs, cr, n_cand}, list_len, k, row_offset, out_s, out_r, rec, gate, rs)
 #define RFX_M(KV)                                                                                     \
   if (kk == KV) {                                                                                     \
     if (rows_are_i64 && sorted)                                                                       \
@@ -291,7 +294,7 @@ int launch_merge_gathered(const void* rec, int world, int64_t nq, int k, float* 
 #define RFX_M(KV)                                                                                     \
   if (kk == KV) {                                                                                     \
     hipLaunchKernelGGL((merge_kernel<KV, true, true, GatheredSrc>), dim3((unsigned)nq), dim3(512), 0, st, \
-                       src, k, k, 0, out_s, out_r, nullptr, nullptr);                                          \
+                       src, k, k, 0, out_s, out_r, nullptr, nullptr, Rescore{});                               \
     return 0;                                                                                         \
   }
   RFX_VALU_K_LIST(RFX_M)

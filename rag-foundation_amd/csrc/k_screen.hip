@@ -219,6 +219,16 @@ __global__ __launch_bounds__(256) void screen_queries_kernel(const uint16_t* __r
 // ---- select: survivors, exact re-score, top-k (one 512-thread block per query) --------------------
 constexpr int kSelCap = 2048;  // kept candidates per query held in LDS; more -> fallback
 
+#ifdef RFX_DEBUG_BUILD
+// debug library only: per block (query < 256) the 100-MHz wall clock at the select's phase ends
+// (tools/select_phases.py via rfx_dbg_select_times)
+__device__ unsigned long long g_sel_t[256][8];
+#define RFX_SEL_T(i)                                  \
+  if (threadIdx.x == 0 && blockIdx.x < 256) g_sel_t[blockIdx.x][i] = wall_clock64();
+#else
+#define RFX_SEL_T(i)
+#endif
+
 template <int DT, int D>
 __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restrict__ cs, const int* __restrict__ cr,
                                                             const uint32_t* __restrict__ drops, int64_t n_lists,
@@ -229,22 +239,31 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
                                                             Rec* __restrict__ out_rec, uint32_t* __restrict__ gate,
                                                             int* __restrict__ diag, int force) {
   // U1: candidate entries per thread per round (config 3: 512 lists x 10 = 5,120 = one round, rows
-  // loaded with the scores, and the drops with them: one memory round trip instead of four);
-  // U: survivor rows per wave per round of the exact re-score
-  constexpr int NT = 512, NW = NT / 64, NM = D / 256, U = 8, U1 = 10;
+  // loaded with the scores, and the drops with them: one memory round trip instead of four).
+  // The exact re-score: 16 lanes per survivor row (CPL 16-B chunks of the row per lane), U rows per
+  // 16-lane group in flight: 8 waves x 4 groups x U = 96 rows per round (config 3: 94 survivors on
+  // average, so one round, one memory latency)
+  constexpr int NT = 512, NW = NT / 64, CPL = D / 128, U = 3, U1 = 10, RPR = NW * 4 * U;
   __shared__ float ca[kSelCap];   // screen score A of kept candidate i
   __shared__ int crow[kSelCap];   // its row
-  __shared__ int sv[kSelCap];     // survivor j -> candidate index
-  __shared__ double sx[kSelCap];  // survivor j's exact score
-  __shared__ int srow[kSelCap];   // survivor j's row (the rank loop reads it without the sv -> crow hop)
+  __shared__ float sx[kSelCap];   // survivor j's exact score: fl32 of the f64 sum (the two-pass rule)
+  __shared__ int srow[kSelCap];   // survivor j's row
+  __shared__ float res_s[64];     // the answer, written out by one wave
+  __shared__ int res_r[64];
   __shared__ int n_c, n_sv, n_ok, fail;
   __shared__ float ak;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int64_t q = blockIdx.x;
+  RFX_SEL_T(0)
   if (tid == 0) {
     n_c = n_sv = n_ok = fail = 0;
     ak = -__builtin_inff();
   }
+  // the query's row chunks for the re-score (16-lane layout below), loaded with everything else
+  const int gl = lane & 15, grp = w * 4 + (lane >> 4);
+  uint4 yq[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) yq[c] = *(const uint4*)(Q + q * D + (gl + 16 * c) * 8);
   __syncthreads();
   // 1. compact the kept candidates (the scan wrote -inf for empty slots and dropped entries)
   const int64_t n = n_lists * list_len;
@@ -271,6 +290,7 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
       }
   }
   __syncthreads();
+  RFX_SEL_T(1)
   const int nc = n_c;
   if (nc > kSelCap || force) fail = 1;
   const int ncl = nc < kSelCap ? nc : kSelCap;
@@ -287,6 +307,7 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
     if (gt < k && ge >= k) ak = si;  // every writer writes the same value
   }
   __syncthreads();
+  RFX_SEL_T(2)
   const float e2 = qe2[q];
   const float t = ncl >= k ? ak - e2 : -__builtin_inff();
   const uint32_t ot = ord(t);
@@ -297,8 +318,9 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
     if (d && d >= ot) fail = 1;
   }
   for (int i = tid; i < ncl; i += NT)
-    if (ca[i] >= t) sv[atomicAdd(&n_sv, 1)] = i;
+    if (ca[i] >= t) srow[atomicAdd(&n_sv, 1)] = crow[i];
   __syncthreads();
+  RFX_SEL_T(3)
   if (fail) {
     if (tid == 0) __hip_atomic_store(gate, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (diag && tid == 0) {
@@ -308,84 +330,86 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
     return;  // the gated exact pass rewrites the whole batch
   }
   const int ns = n_sv;
-  // 4. exact re-score: lane holds query elements 256 m + 4 lane + e; f32 products of bf16 / f16
-  // values are exact, their sum is taken in f64 (the oracle's f64 dot up to f64 rounding)
-  float y[NM][4];
-#pragma unroll
-  for (int m = 0; m < NM; ++m) {
-    const uint2 v = *(const uint2*)(Q + q * D + 256 * m + 4 * lane);
-    const uint32_t u[2] = {v.x, v.y};
-#pragma unroll
-    for (int e = 0; e < 4; ++e) y[m][e] = widen<DT>((uint16_t)(e & 1 ? u[e >> 1] >> 16 : u[e >> 1] & 0xffffu));
-  }
-  for (int j0 = w; j0 < ns; j0 += NW * U) {
-    uint2 xv[U][NM];
+  // 4. exact re-score: the 16 lanes of a group hold chunks gl + 16 c of the row (8 elements each); f32
+  // products of bf16 / f16 values are exact, their sum is taken in f64 (the oracle's f64 dot up to
+  // f64 rounding), rounded once to f32
+  for (int j0 = grp; j0 < ns; j0 += RPR) {
+    uint4 xv[U][CPL];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int j = j0 + u * NW;
-      const int64_t row = j < ns ? (int64_t)crow[sv[j]] : 0;
+      const int j = j0 + u * NW * 4;
+      const int64_t row = j < ns ? (int64_t)srow[j] : (int64_t)srow[0];
 #pragma unroll
-      for (int m = 0; m < NM; ++m) xv[u][m] = *(const uint2*)(X + row * D + 256 * m + 4 * lane);
+      for (int c = 0; c < CPL; ++c) xv[u][c] = *(const uint4*)(X + row * D + (gl + 16 * c) * 8);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       double acc = 0.0;
 #pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        const uint32_t uu[2] = {xv[u][m].x, xv[u][m].y};
+      for (int c = 0; c < CPL; ++c) {
+        const uint32_t xx[4] = {xv[u][c].x, xv[u][c].y, xv[u][c].z, xv[u][c].w};
+        const uint32_t yy[4] = {yq[c].x, yq[c].y, yq[c].z, yq[c].w};
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          acc += (double)(widen<DT>((uint16_t)(e & 1 ? uu[e >> 1] >> 16 : uu[e >> 1] & 0xffffu)) * y[m][e]);
+        for (int e = 0; e < 8; ++e) {
+          const uint16_t xh = (uint16_t)(e & 1 ? xx[e >> 1] >> 16 : xx[e >> 1] & 0xffffu);
+          const uint16_t yh = (uint16_t)(e & 1 ? yy[e >> 1] >> 16 : yy[e >> 1] & 0xffffu);
+          acc += (double)(widen<DT>(xh) * widen<DT>(yh));
+        }
       }
 #pragma unroll
-      for (int off = 32; off; off >>= 1) acc += __shfl_xor(acc, off);
-      const int j = j0 + u * NW;
-      if (lane == 0 && j < ns) {
-        sx[j] = acc;
-        srow[j] = crow[sv[j]];
-      }
+      for (int off = 8; off; off >>= 1) acc += __shfl_xor(acc, off);  // within the 16-lane group
+      const int j = j0 + u * NW * 4;
+      if (gl == 0 && j < ns) sx[j] = (float)acc;
     }
   }
   __syncthreads();
-  // 5. top-k of the survivors by (exact score desc, row asc); NaN (cannot occur for live rows) last
+  RFX_SEL_T(4)
+  // 5. top-k of the survivors by (exact score desc, row asc) with the exact score rounded to f32 first
+  // (the order every merge of f32 scores keeps: a sharded store's gathered merge, kernel 11); NaN
+  // (cannot occur for live rows) last.  The k best land in LDS; one wave writes them out.
   for (int j = tid; j < ns; j += NT) {
-    const double sj = sx[j];
+    const float sj = sx[j];
     if (sj != sj) continue;
     const int rj = srow[j];
     int rank = 0;
 #pragma unroll 8
     for (int i = 0; i < ns; ++i) {
-      const double si = sx[i];
+      const float si = sx[i];
       rank += si > sj || (si == sj && srow[i] < rj);
     }
     atomicAdd(&n_ok, 1);
     if (rank < k) {
-      const float sf = (float)sj;
-      const long long rr = (long long)rj + row_offset;
-      if (out_rec)
-        out_rec[q * k + rank] = Rec{sf, 0, rr};
-      else {
-        out_s[q * k + rank] = sf;
-        out_r[q * k + rank] = rr;
-      }
+      res_s[rank] = sj;
+      res_r[rank] = rj;
     }
   }
+  RFX_SEL_T(6)
   __syncthreads();
-  for (int i = n_ok + tid; i < k; i += NT) {
-    if (out_rec)
-      out_rec[q * k + i] = Rec{-__builtin_inff(), 0, -1};
-    else {
-      out_s[q * k + i] = -__builtin_inff();
-      out_r[q * k + i] = -1;
+  if (tid < k) {
+    const bool ok = tid < n_ok;
+    const float sf = ok ? res_s[tid] : -__builtin_inff();
+    const long long rr = ok ? (long long)res_r[tid] + row_offset : -1;
+    if (out_rec) {
+      out_rec[q * k + tid] = Rec{sf, 0, rr};
+    } else {
+      out_s[q * k + tid] = sf;
+      out_r[q * k + tid] = rr;
     }
   }
   if (diag && tid == 0) {
     diag[q * 2] = nc;
     diag[q * 2 + 1] = ns;
   }
+  RFX_SEL_T(5)
 }
 
 }  // namespace
+
+#ifdef RFX_DEBUG_BUILD
+int dbg_select_times(unsigned long long* out_h) {
+  return hipMemcpyFromSymbol(out_h, HIP_SYMBOL(g_sel_t), sizeof(g_sel_t)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // ---- host launchers --------------------------------------------------------------------------------
 // the int8 copy: bf16 / f16 / f32 stores at d 768 / 1024 (kernel 10 screens bf16 / f16 batches,

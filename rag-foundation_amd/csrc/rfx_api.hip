@@ -506,15 +506,17 @@ int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t
                               scr, drops, st, mask) != 0)
     return fail(RFX_EUNSUPPORTED, "screen scan launch rejected");
   if (ev1) RFX_HIP(hipEventRecord((hipEvent_t)ev1, st));
-  if (rfx::launch_screen_select(scs, scr, drops, L.sp.n_lists, L.sp.k_lane, qe2, queries, ix.data, ix.dim, ix.dtype, nq,
-                                k, row_offset, out_s, out_r, out_rec, gate, diag, ix.screen == 2, st) != 0)
-    return fail(RFX_EUNSUPPORTED, "screen select k=%d unsupported", k);
-  // gated exact pass (no work unless the select kernel set the gate)
+  // the select and the gated exact pass read the queries with 16-B loads: an unaligned batch (or one
+  // that is not a whole number of the fallback's query groups) is copied once into the workspace
   const void* qpad = queries;
   if (nq != L.mp.nq_pad || ((uintptr_t)queries & 15)) {
     qpad = ws + L.q_off;
     rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, 2, (void*)qpad, st);
   }
+  if (rfx::launch_screen_select(scs, scr, drops, L.sp.n_lists, L.sp.k_lane, qe2, qpad, ix.data, ix.dim, ix.dtype, nq,
+                                k, row_offset, out_s, out_r, out_rec, gate, diag, ix.screen == 2, st) != 0)
+    return fail(RFX_EUNSUPPORTED, "screen select k=%d unsupported", k);
+  // gated exact pass (no work unless the select kernel set the gate)
   float* cs = (float*)(ws + L.cs_off);
   int32_t* cr = (int32_t*)(ws + L.cr_off);
   const int rc = L.fbk == 6 ? rfx::launch_scan_mfma6(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs,
@@ -522,8 +524,10 @@ int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t
                             : rfx::launch_scan_mfma8(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs,
                                                      cr, st, mask, gate, ftau);
   if (rc != 0) return fail(RFX_EUNSUPPORTED, "fallback scan launch rejected (%d)", rc);
+  // (the fallback's final top-k re-scored by the two-pass rule: the same bits as the select's answer)
+  const rfx::Rescore rs{ix.data, queries, ix.dim, ix.dtype};
   if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.n_cand, L.mp.k_lane, k, row_offset, out_rec ? nullptr : out_s,
-                                   out_rec ? nullptr : out_r, out_rec, st, /*sorted=*/true, gate) != 0)
+                                   out_rec ? nullptr : out_r, out_rec, st, /*sorted=*/true, gate, &rs) != 0)
     return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
   RFX_HIP(hipGetLastError());
   return RFX_OK;
@@ -1142,6 +1146,7 @@ int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k
 
 }  // extern "C"
 namespace rfx {
+int dbg_select_times(unsigned long long* out_h);
 constexpr int k10_tau_words() { return 16; }  // k_scan_screen.h kTauW
 int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, const void* tmv, const uint32_t* sts,
                            int nrows, const int8_t* Qc, const float* qe2, int nq, uint32_t* tau, float* cs, int* cr,
@@ -1149,7 +1154,7 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
 }
 extern "C" {
 // Diagnostic (k10_dbg.hip): the two-pass scan's query quantiser + one kernel-10 variant
-// (100 * RING + MODE), or variant 9: a plain streaming read of the int8 copy (its HBM ceiling).
+// (100000 * RING + MODE), or variant 9: a plain streaming read of the int8 copy (its HBM ceiling).
 int rfx_dbg_screen_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k, int variant, void* ws_d,
                            size_t ws_bytes, void* stream) {
   auto ix = get(h);
@@ -1192,6 +1197,15 @@ int rfx_dbg_screen_counts(rfx_index_t h, int64_t nq, int k, const void* ws_d, ui
   uint64_t n = 0;
   for (size_t q = 0; q < (size_t)L.sp.nq_pad; ++q) n += t[q * rfx::k10_tau_words() + 15];
   *out = n;
+  return RFX_OK;
+}
+
+// Diagnostic: the select kernel's per-block phase clocks of its last launch (k_screen.hip g_sel_t:
+// [256][8] u64, 100-MHz wall clock; phases 0 start, 1 candidates compacted, 2 a_k, 3 survivors,
+// 4 re-scored, 5 written).
+int rfx_dbg_select_times(unsigned long long* out_h) {
+  if (!out_h) return fail(RFX_EINVAL, "null out");
+  if (rfx::dbg_select_times(out_h) != 0) return fail(RFX_EDEVICE, "hipMemcpyFromSymbol failed");
   return RFX_OK;
 }
 

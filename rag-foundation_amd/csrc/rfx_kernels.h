@@ -7,6 +7,13 @@
 #include "../../include/rfx.h"
 
 namespace rfx {
+// f64 re-score of a two-pass fallback's final top-k (k_scan_valu.h rescore_final)
+struct Rescore {
+  const void* X = nullptr;  // the index rows [rows][D] (dtype); nullptr = no re-score
+  const void* Q = nullptr;  // the queries [nq][D] in the index dtype
+  int D = 0;
+  int dtype = 0;
+};
 
 // ---- generator / maintenance -------------------------------------------------------------
 void launch_synth_rows(uint64_t seed, int64_t row0, int64_t n, int dim, int dtype, void* out,
@@ -122,7 +129,7 @@ int launch_topk_merge(const float* cs, const void* cr, int rows_are_i64, int64_t
 int launch_topk_merge_lists(const float* cs, const void* cr, int rows_are_i64, int64_t nq, int64_t n_cand,
                             int list_len, int k, int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec,
                             hipStream_t st,
-                            bool sorted = false, const uint32_t* gate = nullptr);
+                            bool sorted = false, const uint32_t* gate = nullptr, const Rescore* rescore = nullptr);
 int launch_merge_gathered(const void* rec, int world, int64_t nq, int k, float* out_s, int64_t* out_r,
                           hipStream_t st);
 // n (score, row) pairs -> {score, 0, row + row_offset} merge records (rec) or (out_s, out_r + row_offset);

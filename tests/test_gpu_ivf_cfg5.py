@@ -102,10 +102,14 @@ def test_cfg5_recall_vs_oracle_bruteforce(cfg5):
     rec = lambda rr: float(np.mean([len(set(rr[i].tolist()) & set(exact[j].tolist())) / K for j, i in enumerate(sel)]))
     r_ivf, r_rr = r_ivf.cpu().numpy(), r_rr.cpu().numpy()
     print(f"cfg5 recall@{K}: ivf {rec(r_ivf):.4f}  rerank {rec(r_rr):.4f}")
-    # measured (round 3, this corpus and training): ivf 0.8625, rerank 0.8719 — the misses are rows
-    # in lists outside the 32 probed (a quality property of IVF, not a parity one); the floor below
-    # catches a broken probe / list build, which drops recall far lower
-    assert rec(r_ivf) >= 0.8 and rec(r_rr) >= rec(r_ivf), (rec(r_ivf), rec(r_rr))
+    # measured (round 3, profiles/r03j_pytest_cfg5.log; the run is deterministic — every stage is
+    # bit-exact with oracle/ivf.py): ivf 0.8625, rerank 0.8719.  The misses are rows in lists outside the
+    # 32 probed (a quality property of IVF at this training, not a parity one).  Floors: the measured
+    # values minus 0.01 (a 10-point regression must fail)
+    recipe = (f"training recipe: k-means on every {TRAIN_STEP}th row ({N // TRAIN_STEP} rows), {ITERS} iterations, "
+              f"nlist {NLIST}, nprobe {NPROBE}, clustered corpus CSEED={CSEED} CENTRES={CENTRES}")
+    assert rec(r_ivf) >= 0.8525, (rec(r_ivf), "list search below 0.8625 - 0.01;", recipe)
+    assert rec(r_rr) >= 0.8619 and rec(r_rr) >= rec(r_ivf), (rec(r_rr), "re-rank below 0.8719 - 0.01;", recipe)
 
 
 @pytest.mark.timeout(600)
@@ -156,6 +160,9 @@ def test_cfg5_through_ivf_store(cfg5, tmp_path):
     r_ivf = r_ivf.cpu().numpy()
     rec_ivf = float(np.mean([len(set(r_ivf[i].tolist()) & set(exact[j].tolist())) / K for j, i in enumerate(sel)]))
     print(f"cfg5 store recall@{K}: {rec:.4f} (list search {rec_ivf:.4f})")
-    assert rec >= 0.85 and rec >= rec_ivf, (rec, rec_ivf)
+    # measured (round 3, commit 7759069; deterministic): store 0.958, list search 0.944 at this training
+    # (the writer's strided 262,144-row sample, 10 iterations, nprobe 32, re-rank of 20 candidates)
+    assert rec >= 0.95 and rec >= rec_ivf, (rec, rec_ivf, "store recall below 0.95 (measured 0.958)")
+    assert rec_ivf >= 0.934, (rec_ivf, "list search below 0.944 - 0.01")
     ref.close()
     reg.drop(st.name)
