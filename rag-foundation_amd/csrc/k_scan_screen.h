@@ -125,10 +125,15 @@ __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b)
 // scan, and each lane inserts its passing values one per trip (KL independent compares, no memory).  The serial LDS insert (one dependent
 // LDS round trip per shifted entry) is debug MODE 1024: a wave in this slow path holds the whole
 // workgroup at the next stage barrier.
-template <int KL, bool REG = true>
+// Debug MODE 4096 (append ablation, timing only): after the first kAppW tiles a passing value is
+// appended to a per-lane buffer of kAppC keys (no sorted insert) while it has room; the own list no
+// longer tightens (the bound then comes from the slot table).
+constexpr int kAppC = 6, kAppW = 8;
+template <int KL, bool REG = true, bool APP = false>
 __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint32_t bits, uint64_t* Ls, uint64_t (&L)[KL],
                                             uint32_t& thr_o,
-                                            float e2, uint32_t& drop_o, int rbase, v4i32 tau_rsrc, uint32_t slot_voff) {
+                                            float e2, uint32_t& drop_o, int rbase, v4i32 tau_rsrc, uint32_t slot_voff,
+                                            uint64_t (&Ap)[kAppC], int& an, bool app_now) {
   int mx = max3i(a[0][0], a[0][1], a[0][2]);
   mx = max3i(mx, a[0][3], a[1][0]);
   mx = max3i(mx, a[1][1], a[1][2]);
@@ -172,6 +177,14 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
         // falls out as 0, which max ignores).  KL independent compares, no branch: the list stays in
         // the same registers from trip to trip.
         const uint64_t key = ((uint64_t)ord(s) << 32) | (uint32_t)(~(uint32_t)row);
+        if constexpr (APP) {
+          if (app_now && an < kAppC) {
+#pragma unroll
+            for (int jj = 0; jj < kAppC; ++jj) Ap[jj] = an == jj ? key : Ap[jj];
+            ++an;
+            continue;
+          }
+        }
         bool c[KL];
 #pragma unroll
         for (int i = 0; i < KL; ++i) c[i] = L[i] > key;
@@ -183,7 +196,12 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
       }
       const uint32_t own = (uint32_t)(L[KL - 1] >> 32);
       thr_o = own > thr_o ? own : thr_o;
-      batomic_umax(tau_rsrc, slot_voff, (uint32_t)(L[0] >> 32));
+      uint64_t best = L[0];
+      if constexpr (APP) {
+#pragma unroll
+        for (int jj = 0; jj < kAppC; ++jj) best = Ap[jj] > best ? Ap[jj] : best;
+      }
+      batomic_umax(tau_rsrc, slot_voff, (uint32_t)(best >> 32));
     } else {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -226,7 +244,8 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
 // 256 = kernel 6's slot-table bound (min over KL slots) instead of the KL-th largest of 16, 512 = the
 // slow path compiled in but never taken (wrong results; separates its cost from the code's presence),
 // 1024 = the slow path's serial LDS list insert instead of the register-resident list, 16 = the slot
-// table re-read at every one of the first 16 tiles, 2048 = issue priority for a wave in the slow path.
+// table re-read at every one of the first 16 tiles, 2048 = issue priority for a wave in the slow path,
+// 4096 = append instead of insert after the first kAppW tiles (timing only).
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
@@ -270,6 +289,10 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   uint64_t Lr[KL];  // production: the lane's list lives in registers for the whole scan
 #pragma unroll
   for (int i = 0; i < KL; ++i) Lr[i] = 0ull;
+  uint64_t Ap[kAppC];  // debug MODE 4096's append buffer
+  int an = 0;
+#pragma unroll
+  for (int i = 0; i < kAppC; ++i) Ap[i] = 0ull;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -434,8 +457,9 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
             acc4[2 * rb][i] = (int)r[0];
             acc4[2 * rb + 1][i] = (int)r[1];
           }
-        fold_screen<KL, (MODE & 1024) == 0>(acc4, st, lw >> (8 * half), Ls, Lr, thr, e2, drop, tile * kTM + 8 * half,
-                                            tau_rsrc, slot_voff);
+        fold_screen<KL, (MODE & 1024) == 0, (MODE & 4096) != 0>(acc4, st, lw >> (8 * half), Ls, Lr, thr, e2, drop,
+                                                                 tile * kTM + 8 * half, tau_rsrc, slot_voff, Ap, an,
+                                                                 it >= kAppW);
         set_bounds();
         if constexpr ((MODE & 2048) != 0) __builtin_amdgcn_s_setprio(0);
       }
@@ -555,7 +579,12 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
       cand_s[o + i] = keep ? sc : -__builtin_inff();
       cand_r[o + i] = keep ? (int)(~(uint32_t)key) : kEmptyRow;
     }
-    drops[(int64_t)q * n_lists + lst] = drop;
+    uint32_t dr = drop;
+    if constexpr ((MODE & 4096) != 0) {  // (timing only: the appended keys kept live through the drop word)
+#pragma unroll
+      for (int i = 0; i < kAppC; ++i) dr = max(dr, (uint32_t)(Ap[i] >> 32));
+    }
+    drops[(int64_t)q * n_lists + lst] = dr;
   }
 }
 

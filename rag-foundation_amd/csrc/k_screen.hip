@@ -246,17 +246,18 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
   constexpr int NT = 512, NW = NT / 64, CPL = D / 128, U = 3, U1 = 10, RPR = NW * 4 * U;
   __shared__ float ca[kSelCap];   // screen score A of kept candidate i
   __shared__ int crow[kSelCap];   // its row
-  __shared__ float sx[kSelCap];   // survivor j's exact score: fl32 of the f64 sum (the two-pass rule)
   __shared__ int srow[kSelCap];   // survivor j's row
-  __shared__ float res_s[64];     // the answer, written out by one wave
-  __shared__ int res_r[64];
-  __shared__ int n_c, n_sv, n_ok, fail;
+  // survivor j's rank key: (orderable fl32 of the exact f64 sum) << 32 | ~row — larger key = better
+  // under (score desc, row asc), so a rank is one 64-bit compare per survivor, no branches
+  __shared__ uint64_t skey[kSelCap];
+  __shared__ uint64_t res_key[64];  // the answer, written out by one wave
+  __shared__ int n_c, n_sv, fail;
   __shared__ float ak;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int64_t q = blockIdx.x;
   RFX_SEL_T(0)
   if (tid == 0) {
-    n_c = n_sv = n_ok = fail = 0;
+    n_c = n_sv = fail = 0;
     ak = -__builtin_inff();
   }
   // the query's row chunks for the re-score (16-lane layout below), loaded with everything else
@@ -359,7 +360,7 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
 #pragma unroll
       for (int off = 8; off; off >>= 1) acc += __shfl_xor(acc, off);  // within the 16-lane group
       const int j = j0 + u * NW * 4;
-      if (gl == 0 && j < ns) sx[j] = (float)acc;
+      if (gl == 0 && j < ns) skey[j] = ((uint64_t)ord((float)acc) << 32) | (uint32_t)(~(uint32_t)srow[j]);
     }
   }
   __syncthreads();
@@ -368,27 +369,19 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
   // (the order every merge of f32 scores keeps: a sharded store's gathered merge, kernel 11); NaN
   // (cannot occur for live rows) last.  The k best land in LDS; one wave writes them out.
   for (int j = tid; j < ns; j += NT) {
-    const float sj = sx[j];
-    if (sj != sj) continue;
-    const int rj = srow[j];
+    const uint64_t kj = skey[j];
     int rank = 0;
 #pragma unroll 8
-    for (int i = 0; i < ns; ++i) {
-      const float si = sx[i];
-      rank += si > sj || (si == sj && srow[i] < rj);
-    }
-    atomicAdd(&n_ok, 1);
-    if (rank < k) {
-      res_s[rank] = sj;
-      res_r[rank] = rj;
-    }
+    for (int i = 0; i < ns; ++i) rank += skey[i] > kj ? 1 : 0;
+    if (rank < k) res_key[rank] = kj;
   }
   RFX_SEL_T(6)
   __syncthreads();
   if (tid < k) {
-    const bool ok = tid < n_ok;
-    const float sf = ok ? res_s[tid] : -__builtin_inff();
-    const long long rr = ok ? (long long)res_r[tid] + row_offset : -1;
+    const bool ok = tid < ns;  // (survivors are live rows: never NaN)
+    const uint64_t kk = ok ? res_key[tid] : 0ull;
+    const float sf = ok ? unord((uint32_t)(kk >> 32)) : -__builtin_inff();
+    const long long rr = ok ? (long long)(int)(~(uint32_t)kk) + row_offset : -1;
     if (out_rec) {
       out_rec[q * k + tid] = Rec{sf, 0, rr};
     } else {

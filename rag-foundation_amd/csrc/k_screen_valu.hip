@@ -294,7 +294,9 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   __shared__ float bs[kFusedLdsCand];
   __shared__ int br[kFusedLdsCand];
   __shared__ int sv[kSurvCap];    // survivor -> record index
-  __shared__ float sx[kSurvCap];  // its exact score
+  // its rank key: (orderable fl32 of the exact f64 sum) << 32 | ~row, larger = better under (score
+  // desc, row asc): the rank is one 64-bit compare per survivor (no branches, no dependent LDS loads)
+  __shared__ uint64_t skey[kSurvCap];
   __shared__ float red[4];
   __shared__ int n_sv, fail;
   __shared__ float cut;
@@ -414,18 +416,20 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
         }
 #pragma unroll
         for (int off = 4; off; off >>= 1) acc += __shfl_xor(acc, off);  // within the 8-lane group
-        if (gl == 0 && e < ns) sx[e] = (float)acc;
+        if (gl == 0 && e < ns)
+          skey[e] = ((uint64_t)ord_f32((float)acc) << 32) | (uint32_t)(~(uint32_t)br[sv[e]]);
       }
       __syncthreads();
       // top-k of the survivors by (exact score desc, row asc): each survivor counts those ahead of it
       for (int e = tid; e < ns; e += 256) {
-        const float se = sx[e];
-        const int re = br[sv[e]];
+        const uint64_t ke = skey[e];
         int rank = 0;
-        for (int f = 0; f < ns; ++f) rank += better(sx[f], br[sv[f]], se, re);
+#pragma unroll 8
+        for (int f = 0; f < ns; ++f) rank += skey[f] > ke ? 1 : 0;
         if (rank < k_out) {
-          out_s[(int64_t)qi * k_out + rank] = se;
-          out_r[(int64_t)qi * k_out + rank] = re;
+          const uint32_t o = (uint32_t)(ke >> 32);
+          out_s[(int64_t)qi * k_out + rank] = __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+          out_r[(int64_t)qi * k_out + rank] = (int)(~(uint32_t)ke);
         }
       }
       for (int i = ns + tid; i < k_out; i += 256) {  // fewer survivors than k: padding
