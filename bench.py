@@ -145,7 +145,7 @@ def main():
 
     from rfx import dist as rdist
     from rfx._lib import RfxCapacityError
-    from rfx.index import DeviceIndex, merge_gathered, synth_rows
+    from rfx.index import DeviceIndex, synth_rows
 
     comm, exchange_note = None, None
     multi = world > 1 or a.force_comm  # the sharded step: records -> all-gather -> gathered merge
@@ -217,6 +217,8 @@ def main():
 
     out_s = torch.empty((a.nq, a.k), dtype=torch.float32, device=dev)
     out_r = torch.empty((a.nq, a.k), dtype=torch.int64, device=dev)
+    mg_s = torch.empty((a.nq, a.k), dtype=torch.float32, device=dev)  # the gathered merge's answer (N > 1)
+    mg_r = torch.empty((a.nq, a.k), dtype=torch.int64, device=dev)
     NEV = 5  # scan begin, scan end, search done (records / result), all-gather done, gathered merge done
 
     def new_events():
@@ -259,10 +261,10 @@ def main():
                 g = torch.stack(parts).to(dev)
         if ev is not None:
             ev[3].record(stream)
-        res = merge_gathered(g, a.k, stream=stream)
+        check(lib.rfx_merge_gathered(ptr(g), world, a.nq, a.k, ptr(mg_s), ptr(mg_r), stream_ptr(stream)))
         if ev is not None:
             ev[4].record(stream)
-        return res
+        return mg_s, mg_r
 
     for i in range(a.warmup):
         step(i)
@@ -274,6 +276,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         out = step(i, evs.get(i))
+    host_issue = time.perf_counter() - t0  # host time to enqueue the K steps (GPU-bound when < elapsed)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -361,6 +364,7 @@ def main():
                      "kernel_ms": round(scan_ms, 4), "event_timed_launches": len(evs),
                      "alg_bytes_per_launch": alg_bytes},
         "phases_ms": {k_: round(v, 4) for k_, v in phases.items()},
+        "host_issue_ms_per_step": round(host_issue / a.steps * 1e3, 4),
     }
     if comm is not None:
         result["config"]["rccl"] = {"world": comm.world, "rank_of_reporter": comm.rank, "n_local": comm.n_local}

@@ -121,19 +121,16 @@ __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b)
 // Fold one tile's 16 values of this lane (rows rbase + (r & 7) + 16 (r >> 3), ROWMAP 1 of
 // k_mfma_common.h) into its list.  thr_o: the pruning bound (orderable A, 0 = none); rows are
 // looked at from thr − e2 on.  drop_o: the best A this lane looked at and did not keep.
-// Production: the 16 pass tests make a bit mask first; the list (L) lives in registers for the whole
-// scan, and each lane inserts its passing values one per trip (KL independent compares, no memory).  The serial LDS insert (one dependent
-// LDS round trip per shifted entry) is debug MODE 1024: a wave in this slow path holds the whole
-// workgroup at the next stage barrier.
-// Debug MODE 4096 (append ablation, timing only): after the first kAppW tiles a passing value is
-// appended to a per-lane buffer of kAppC keys (no sorted insert) while it has room; the own list no
-// longer tightens (the bound then comes from the slot table).
-constexpr int kAppC = 6, kAppW = 8;
-template <int KL, bool REG = true, bool APP = false>
-__device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint32_t bits, uint64_t* Ls, uint64_t (&L)[KL],
-                                            uint32_t& thr_o,
-                                            float e2, uint32_t& drop_o, int rbase, v4i32 tau_rsrc, uint32_t slot_voff,
-                                            uint64_t (&Ap)[kAppC], int& an, bool app_now) {
+// Production: the 16 pass tests make a bit mask first (fold_mask); the list (L) lives in registers for
+// the whole scan, and each lane inserts its passing values one per trip (fold_trip: KL independent
+// compares, no memory); fold_end tightens the own bound and publishes the list's best.  The kernel runs
+// the trips deferred, one per k-step of the next tile, under that tile's MFMAs (DEFER below).  The
+// serial LDS insert (one dependent LDS round trip per shifted entry) is debug MODE 1024: a wave in this
+// slow path holds the whole workgroup at the next stage barrier.
+// The pass mask: bit r set = value r is live and reaches thr − e2; pub = the tile's best reaches it (the
+// lane then publishes its list's best, fold_end).
+__device__ __forceinline__ uint32_t fold_mask(const v4i32 (&a)[4], float st, uint32_t bits, uint32_t thr_o, float e2,
+                                              bool& pub) {
   int mx = max3i(a[0][0], a[0][1], a[0][2]);
   mx = max3i(mx, a[0][3], a[1][0]);
   mx = max3i(mx, a[1][1], a[1][2]);
@@ -143,91 +140,99 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
   mx = max3i(mx, a[3][1], a[3][2]);
   mx = max(mx, a[3][3]);
   const float thr = thr_o ? unord(thr_o) - e2 : -__builtin_inff();
-  if ((float)mx * st >= thr) {  // s_t >= 0: the tile's best A bounds every row's
-    if constexpr (REG) {
-      // which of the 16 values pass (live bits applied once, re-ordered to r: bit r <- row bit
-      // (r & 7) + 16 (r >> 3)), without branching on each one
-      uint32_t pm = 0;
+  pub = (float)mx * st >= thr;  // s_t >= 0: the tile's best A bounds every row's
+  uint32_t pm = 0;
+  if (pub) {
+    // which of the 16 values pass (live bits applied once, re-ordered to r: bit r <- row bit
+    // (r & 7) + 16 (r >> 3)), without branching on each one
 #pragma unroll
-      for (int r = 0; r < 16; ++r) pm |= (float)a[r >> 2][r & 3] * st >= thr ? (1u << r) : 0u;
-      pm &= (bits & 0xffu) | ((bits >> 8) & 0xff00u);
-      // one passing value per lane per trip: the wave makes max-over-lanes(popcount) trips, not one
-      // trip per position some lane passes at
-      while (pm) {
-        const int r = __builtin_ctz(pm);
-        pm &= pm - 1;
-        // value r: a select tree on r's bits as bit-field inserts (15 v_bfi_b32); the masks go through
-        // an empty asm so the compiler cannot turn the tree back into an indexed (scratch) read of a
-        int m3 = -((r >> 3) & 1), m2 = -((r >> 2) & 1), m1 = -((r >> 1) & 1), m0 = -(r & 1);
-        asm volatile("" : "+v"(m3), "+v"(m2), "+v"(m1), "+v"(m0));
-        int v[8];
+    for (int r = 0; r < 16; ++r) pm |= (float)a[r >> 2][r & 3] * st >= thr ? (1u << r) : 0u;
+    pm &= (bits & 0xffu) | ((bits >> 8) & 0xff00u);
+  }
+  return pm;
+}
+// One passing value of this lane (the lowest bit of pm, cleared) into its list.
+template <int KL>
+__device__ __forceinline__ void fold_trip(const v4i32 (&a)[4], float st, int rbase, uint32_t& pm, uint64_t (&L)[KL],
+                                          uint32_t& drop_o) {
+  const int r = __builtin_ctz(pm);
+  pm &= pm - 1;
+  // value r: a select tree on r's bits as bit-field inserts (15 v_bfi_b32); the masks go through
+  // an empty asm so the compiler cannot turn the tree back into an indexed (scratch) read of a
+  int m3 = -((r >> 3) & 1), m2 = -((r >> 2) & 1), m1 = -((r >> 1) & 1), m0 = -(r & 1);
+  asm volatile("" : "+v"(m3), "+v"(m2), "+v"(m1), "+v"(m0));
+  int v[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = (a[(j + 8) >> 2][j & 3] & m3) | (a[j >> 2][j & 3] & ~m3);
+  for (int j = 0; j < 8; ++j) v[j] = (a[(j + 8) >> 2][j & 3] & m3) | (a[j >> 2][j & 3] & ~m3);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = (v[j + 4] & m2) | (v[j] & ~m2);
+  for (int j = 0; j < 4; ++j) v[j] = (v[j + 4] & m2) | (v[j] & ~m2);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) v[j] = (v[j + 2] & m1) | (v[j] & ~m1);
-        const int av = (v[1] & m0) | (v[0] & ~m0);
-        const float s = (float)av * st;
+  for (int j = 0; j < 2; ++j) v[j] = (v[j + 2] & m1) | (v[j] & ~m1);
+  const int av = (v[1] & m0) | (v[0] & ~m0);
+  const float s = (float)av * st;
+  const int row = rbase + (r & 7) + 16 * (r >> 3);
+  // insert, unconditionally and without a dependency chain: with c_i = (L_i > key) and the list
+  // sorted, the new entry i is c_{i-1} ? (c_i ? L_i : key) : L_{i-1} (c_{-1} = true), and the
+  // smallest of L and the key falls out — the evicted entry when the key goes in, the key itself
+  // when it does not; either way a value this lane looked at and did not keep (an empty entry
+  // falls out as 0, which max ignores).  KL independent compares, no branch: the list stays in
+  // the same registers from trip to trip.
+  const uint64_t key = ((uint64_t)ord(s) << 32) | (uint32_t)(~(uint32_t)row);
+  bool c[KL];
+#pragma unroll
+  for (int i = 0; i < KL; ++i) c[i] = L[i] > key;
+  const uint64_t k = c[KL - 1] ? key : L[KL - 1];
+#pragma unroll
+  for (int i = KL - 1; i > 0; --i) L[i] = c[i - 1] ? (c[i] ? L[i] : key) : L[i - 1];
+  L[0] = c[0] ? L[0] : key;
+  drop_o = max(drop_o, (uint32_t)(k >> 32));
+}
+template <int KL>
+__device__ __forceinline__ void fold_end(const uint64_t (&L)[KL], uint32_t& thr_o, bool pub, v4i32 tau_rsrc,
+                                         uint32_t slot_voff) {
+  if (pub) {
+    const uint32_t own = (uint32_t)(L[KL - 1] >> 32);
+    thr_o = own > thr_o ? own : thr_o;
+    batomic_umax(tau_rsrc, slot_voff, (uint32_t)(L[0] >> 32));
+  }
+}
+template <int KL, bool REG = true>
+__device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint32_t bits, uint64_t* Ls, uint64_t (&L)[KL],
+                                            uint32_t& thr_o,
+                                            float e2, uint32_t& drop_o, int rbase, v4i32 tau_rsrc, uint32_t slot_voff) {
+  if constexpr (REG) {
+    bool pub;
+    uint32_t pm = fold_mask(a, st, bits, thr_o, e2, pub);
+    // one passing value per lane per trip: the wave makes max-over-lanes(popcount) trips, not one
+    // trip per position some lane passes at
+    while (pm) fold_trip<KL>(a, st, rbase, pm, L, drop_o);
+    fold_end<KL>(L, thr_o, pub, tau_rsrc, slot_voff);
+  } else {
+    const float thr = thr_o ? unord(thr_o) - e2 : -__builtin_inff();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float s = (float)a[r >> 2][r & 3] * st;
+      if (((bits >> ((r & 7) + 16 * (r >> 3))) & 1u) && s >= thr) {
         const int row = rbase + (r & 7) + 16 * (r >> 3);
-        // insert, unconditionally and without a dependency chain: with c_i = (L_i > key) and the list
-        // sorted, the new entry i is c_{i-1} ? (c_i ? L_i : key) : L_{i-1} (c_{-1} = true), and the
-        // smallest of L and the key falls out — the evicted entry when the key goes in, the key itself
-        // when it does not; either way a value this lane looked at and did not keep (an empty entry
-        // falls out as 0, which max ignores).  KL independent compares, no branch: the list stays in
-        // the same registers from trip to trip.
         const uint64_t key = ((uint64_t)ord(s) << 32) | (uint32_t)(~(uint32_t)row);
-        if constexpr (APP) {
-          if (app_now && an < kAppC) {
-#pragma unroll
-            for (int jj = 0; jj < kAppC; ++jj) Ap[jj] = an == jj ? key : Ap[jj];
-            ++an;
-            continue;
+        const uint64_t last = Ls[(KL - 1) * 64];
+        if (key > last) {
+          if (last) drop_o = max(drop_o, (uint32_t)(last >> 32));  // evicted
+          int i = KL - 1;
+          for (; i > 0; --i) {
+            const uint64_t prev = Ls[(i - 1) * 64];
+            if (prev >= key) break;
+            Ls[i * 64] = prev;
           }
-        }
-        bool c[KL];
-#pragma unroll
-        for (int i = 0; i < KL; ++i) c[i] = L[i] > key;
-        const uint64_t k = c[KL - 1] ? key : L[KL - 1];
-#pragma unroll
-        for (int i = KL - 1; i > 0; --i) L[i] = c[i - 1] ? (c[i] ? L[i] : key) : L[i - 1];
-        L[0] = c[0] ? L[0] : key;
-        drop_o = max(drop_o, (uint32_t)(k >> 32));
-      }
-      const uint32_t own = (uint32_t)(L[KL - 1] >> 32);
-      thr_o = own > thr_o ? own : thr_o;
-      uint64_t best = L[0];
-      if constexpr (APP) {
-#pragma unroll
-        for (int jj = 0; jj < kAppC; ++jj) best = Ap[jj] > best ? Ap[jj] : best;
-      }
-      batomic_umax(tau_rsrc, slot_voff, (uint32_t)(best >> 32));
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float s = (float)a[r >> 2][r & 3] * st;
-        if (((bits >> ((r & 7) + 16 * (r >> 3))) & 1u) && s >= thr) {
-          const int row = rbase + (r & 7) + 16 * (r >> 3);
-          const uint64_t key = ((uint64_t)ord(s) << 32) | (uint32_t)(~(uint32_t)row);
-          const uint64_t last = Ls[(KL - 1) * 64];
-          if (key > last) {
-            if (last) drop_o = max(drop_o, (uint32_t)(last >> 32));  // evicted
-            int i = KL - 1;
-            for (; i > 0; --i) {
-              const uint64_t prev = Ls[(i - 1) * 64];
-              if (prev >= key) break;
-              Ls[i * 64] = prev;
-            }
-            Ls[i * 64] = key;
-          } else {
-            drop_o = max(drop_o, ord(s));  // looked at, not kept
-          }
+          Ls[i * 64] = key;
+        } else {
+          drop_o = max(drop_o, ord(s));  // looked at, not kept
         }
       }
-      const uint32_t own = (uint32_t)(Ls[(KL - 1) * 64] >> 32);
-      thr_o = own > thr_o ? own : thr_o;
-      batomic_umax(tau_rsrc, slot_voff, (uint32_t)(Ls[0] >> 32));
     }
+    const uint32_t own = (uint32_t)(Ls[(KL - 1) * 64] >> 32);
+    thr_o = own > thr_o ? own : thr_o;
+    batomic_umax(tau_rsrc, slot_voff, (uint32_t)(Ls[0] >> 32));
   }
 }
 
@@ -245,7 +250,8 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
 // slow path compiled in but never taken (wrong results; separates its cost from the code's presence),
 // 1024 = the slow path's serial LDS list insert instead of the register-resident list, 16 = the slot
 // table re-read at every one of the first 16 tiles, 2048 = issue priority for a wave in the slow path,
-// 4096 = append instead of insert after the first kAppW tiles (timing only).
+// 16384 = the slow path deferred: its pass mask at the tile's epilogue, its list inserts one per
+// k-step of the next tile (under that tile's MFMAs), the own bound and slot update at its last k-step.
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
@@ -289,10 +295,6 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   uint64_t Lr[KL];  // production: the lane's list lives in registers for the whole scan
 #pragma unroll
   for (int i = 0; i < KL; ++i) Lr[i] = 0ull;
-  uint64_t Ap[kAppC];  // debug MODE 4096's append buffer
-  int an = 0;
-#pragma unroll
-  for (int i = 0; i < kAppC; ++i) Ap[i] = 0ull;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -416,7 +418,16 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   // first k-step of MFMAs (production), so its VALU / LDS work overlaps the matrix cores instead of
   // waiting for the MFMA pipeline to drain at every tile end (debug MODE 128: epilogue in place).
   v4i32 accA[4], accB[4];  // [rb * 2 + qb]
-  auto epilogue = [&](const int it, v4i32(&acc4)[4]) {
+  // The deferred slow path (DEFER): the pass mask of a tile that entered it, the tile's scale and row
+  // base, and whether the lane publishes; the inserts run one per k-step of the next tile, while the
+  // tile's accumulators stay untouched (the next tile accumulates into the other set), and the whole
+  // fold completes at the next tile's last k-step, before any later epilogue reads the bound.
+  constexpr bool DEFER = (MODE & 16384) != 0 && (MODE & (128 | 1024)) == 0;
+  uint32_t pm_p = 0u;
+  float st_p = 0.f;
+  int rb_p = 0;
+  bool pub_p = false, pend = false;
+  auto epilogue = [&](const int it, v4i32(&acc4)[4], const bool defer) {
     const int tile = range + it * nblk;
     // Fast path: the max D of each of the lane's two queries, scaled by the tile's scale, against the
     // query's bound (qb 0 values in acc4[0], acc4[2]; qb 1 in acc4[1], acc4[3]).  Only when some lane of the wave
@@ -457,9 +468,16 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
             acc4[2 * rb][i] = (int)r[0];
             acc4[2 * rb + 1][i] = (int)r[1];
           }
-        fold_screen<KL, (MODE & 1024) == 0, (MODE & 4096) != 0>(acc4, st, lw >> (8 * half), Ls, Lr, thr, e2, drop,
-                                                                 tile * kTM + 8 * half, tau_rsrc, slot_voff, Ap, an,
-                                                                 it >= kAppW);
+        if (DEFER && defer) {
+          pm_p = fold_mask(acc4, st, lw >> (8 * half), thr, e2, pub_p);
+          st_p = st;
+          rb_p = tile * kTM + 8 * half;
+          pend = true;
+          if constexpr ((MODE & 2048) != 0) __builtin_amdgcn_s_setprio(0);
+          return;
+        }
+        fold_screen<KL, (MODE & 1024) == 0>(acc4, st, lw >> (8 * half), Ls, Lr, thr, e2, drop, tile * kTM + 8 * half,
+                                            tau_rsrc, slot_voff);
         set_bounds();
         if constexpr ((MODE & 2048) != 0) __builtin_amdgcn_s_setprio(0);
       }
@@ -530,8 +548,22 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
           for (int qb = 0; qb < 2; ++qb)
             acc4[2 * rb + qb] = ks == 0 ? mfma_i8(cur.a[rb], bq[2 * ks + qb], v4i32{0, 0, 0, 0})
                                         : mfma_i8(cur.a[rb], bq[2 * ks + qb], acc4[2 * rb + qb]);
-        if constexpr ((MODE & 128) == 0)
-          if (s == 0 && kk == 0 && prev) epilogue(it - 1, accp);
+        if constexpr ((MODE & 128) == 0) {
+          if (s == 0 && kk == 0) {
+            if (prev) epilogue(it - 1, accp, true);
+          } else if constexpr (DEFER) {
+            if (pend) {  // (wave-uniform) one insert per lane under this k-step's MFMAs; all of it at the last
+              if (ks < NKS - 1) {
+                if (pm_p) fold_trip<KL>(accp, st_p, rb_p, pm_p, Lr, drop);
+              } else {
+                while (pm_p) fold_trip<KL>(accp, st_p, rb_p, pm_p, Lr, drop);
+                fold_end<KL>(Lr, thr, pub_p, tau_rsrc, slot_voff);
+                set_bounds();
+                pend = false;
+              }
+            }
+          }
+        }
       }
     }
 
@@ -539,7 +571,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   if constexpr ((MODE & 128) != 0) {
     for (int it = 0; it < nt; ++it) {
       tile_body(it, accA, accB, false);
-      epilogue(it, accA);
+      epilogue(it, accA, false);
     }
   } else {
     int it = 0;
@@ -549,9 +581,9 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
     }
     if (it < nt) {
       tile_body(it, accA, accB, it > 0);
-      epilogue(it, accA);
+      epilogue(it, accA, false);
     } else {
-      epilogue(it - 1, accB);
+      epilogue(it - 1, accB, false);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -579,12 +611,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
       cand_s[o + i] = keep ? sc : -__builtin_inff();
       cand_r[o + i] = keep ? (int)(~(uint32_t)key) : kEmptyRow;
     }
-    uint32_t dr = drop;
-    if constexpr ((MODE & 4096) != 0) {  // (timing only: the appended keys kept live through the drop word)
-#pragma unroll
-      for (int i = 0; i < kAppC; ++i) dr = max(dr, (uint32_t)(Ap[i] >> 32));
-    }
-    drops[(int64_t)q * n_lists + lst] = dr;
+    drops[(int64_t)q * n_lists + lst] = drop;
   }
 }
 

@@ -56,6 +56,29 @@ struct Codes {
   uint4 md;  // the row's tile record {scale, live word}, loaded with the codes (prefetched alike)
 };
 
+#ifdef RFX_DEBUG_BUILD
+// debug library only: the 100-MHz wall clock per block (< 1024) at 0 start, 1 query quantised, 2 row
+// stream done, 3 record written; and for the last block 4 records loaded, 5 bound + drop check,
+// 6 survivors, 7 re-scored + ranked (query 0), 8 end (tools/k11_phases.py via rfx_dbg_k11_times)
+__device__ unsigned long long g_k11_t[1024][4];
+__device__ unsigned long long g_k11_last[8];
+#define RFX_K11_T(i) \
+  do {                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 1024) g_k11_t[blockIdx.x][i] = wall_clock64(); \
+  } while (0)
+#define RFX_K11_L(i) \
+  do {                                                   \
+    if (threadIdx.x == 0) g_k11_last[i] = wall_clock64(); \
+  } while (0)
+#else
+#define RFX_K11_T(i) \
+  do {               \
+  } while (0)
+#define RFX_K11_L(i) \
+  do {               \
+  } while (0)
+#endif
+
 template <int DT, int D, int NQT>
 __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restrict__ X8, const uint4* __restrict__ tmeta,
                                                           const uint32_t* __restrict__ stats, int nrows,
@@ -71,6 +94,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   // fallback gate (written by the last block, read by the gated exact search)
   uint32_t* const ctr = state;
   uint32_t* const gate = state + 24;
+  RFX_K11_T(0);
 
   // ---- 1. query codes and e2 (every block, identically): wave w quantises queries w, w + 4 ------
   __shared__ __attribute__((aligned(16))) int8_t qc_lds[NQT][D];
@@ -117,6 +141,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     }
   }
   __syncthreads();
+  RFX_K11_T(1);
   Codes<D> qv[NQT];
 #pragma unroll
   for (int qi = 0; qi < NQT; ++qi)
@@ -228,6 +253,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     }
   }
 
+  RFX_K11_T(2);
   // ---- 3. block record per query: the 15 best A of the block (rows), and its drop bound ----------
   __shared__ float ms[4][NQT][kK];
   __shared__ int mr[4][NQT][kK];
@@ -282,7 +308,9 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     last = old == gridDim.x - 1;
   }
   __syncthreads();
+  RFX_K11_T(3);
   if (!last) return;
+  RFX_K11_L(0);
   if (force & 8) {
     if (tid == 0) {
       *gate = 0u;
@@ -329,6 +357,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     }
     if (tid == 0) n_sv = 0;
     __syncthreads();
+    if (qi == 0) RFX_K11_L(1);
     // The largest drop bound, and LB, a lower bound of a_k from each record's best entry (every entry
     // when the records are few): distinct live rows either way.
     float dmax = -__builtin_inff();
@@ -380,6 +409,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       if (dm_all > -__builtin_inff() && dm_all >= cut) fail = 1;
     }
     __syncthreads();
+    if (qi == 0) RFX_K11_L(2);
     for (int i = tid; i < n; i += 256) {
       const int r = br[i];
       if (r != kEmptyRow && r != kDropRow && bs[i] >= cut) {
@@ -390,6 +420,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     __syncthreads();
     if (n_sv > kSurvCap && tid == 0) fail = 1;
     __syncthreads();
+    if (qi == 0) RFX_K11_L(3);
     if (!fail && !(force & 16)) {
       const int ns = n_sv;
       // exact re-score: 8 lanes per survivor, 32 survivors per round, every row's loads in flight
@@ -438,7 +469,9 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       }
     }
     __syncthreads();
+    if (qi == 0) RFX_K11_L(4);
   }
+  RFX_K11_L(5);
   if (tid == 0) {
     *gate = fail ? 1u : 0u;  // read by the gated exact search that follows on the stream
     *ctr = 0u;
@@ -446,6 +479,13 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
 }
 
 }  // namespace
+
+#ifdef RFX_DEBUG_BUILD
+int dbg_k11_times(unsigned long long* blocks_h, unsigned long long* last_h) {
+  if (hipMemcpyFromSymbol(blocks_h, HIP_SYMBOL(g_k11_t), sizeof(g_k11_t)) != hipSuccess) return -1;
+  return hipMemcpyFromSymbol(last_h, HIP_SYMBOL(g_k11_last), sizeof(g_k11_last)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // One launch: grid (blocks) × 256 threads, one query slice of up to 8 queries.
 int launch_screen_valu(const ValuPlan& p, const int8_t* X8, const void* tmeta, const uint32_t* stats, int nrows, int D,
