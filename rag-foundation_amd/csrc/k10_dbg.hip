@@ -2,7 +2,7 @@
 // two-pass scan's int8 screen (k_scan_screen.h MODE bits: 1 no top-k fold, 2 no launder, 4 prefetch
 // distance 1, 8 no corpus stream, 16 early slot-table refreshes, 32 slow-path entry count, 64 store-wide
 // integer fast-path bound, 128 epilogue in place, 256 min-of-KL slot bound, 512 slow path never taken,
-// 1024 serial LDS insert, 2048 slow-path issue priority, 16384 deferred slow path),
+// 1024 serial LDS insert, 2048 slow-path issue priority, 32768 no stage barriers),
 // via rfx_dbg_screen_variant; variant = 100000 * RING + MODE (RING in {4, 6, 8, 10, 12}).
 #include "k_scan_screen.h"
 
@@ -48,9 +48,9 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
     RFX_K10V(8, 48)
     RFX_K10V(8, 2048)
     RFX_K10V(8, 2080)
-    RFX_K10V(8, 16384)
-    RFX_K10V(8, 16416)
-    RFX_K10V(8, 18432)
+    RFX_K10V(10, 32768)
+    RFX_K10V(10, 32800)
+    RFX_K10V(12, 32768)
     default:
       return -1;
   }

@@ -63,9 +63,25 @@ template <int RING>
 constexpr int tau_off() { return meta_off<RING>() + kMR * 1024; }
 template <int RING>
 constexpr int list_off() { return tau_off<RING>() + kTauBytes; }
+// per-slot arrival counters of the barrier-free ring (debug MODE 32768): ready[16], done[16], in the
+// first 128 B of the debug MODE 1024 list area (never both; both are zeroed before the first barrier)
+template <int KL, int RING>
+constexpr int ctr_off() { return list_off<RING>(); }
 template <int KL, int RING>
 constexpr int lds_bytes() { return list_off<RING>() + kWaves * KL * 64 * 8; }
 static_assert(lds_bytes<10, 12>() <= 163840, "LDS budget");
+
+// spin (s_sleep) until the LDS counter reaches target; bounded, so a counting error can never hang the
+// GPU (the result would be wrong, and the tests would say so)
+__device__ __forceinline__ void lds_spin_ge(const uint32_t* p, uint32_t target) {
+  for (int guard = 0; guard < (1 << 20); ++guard) {
+    if (__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+__device__ __forceinline__ void lds_arrive(uint32_t* p) {
+  __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 static_assert(kSlot / 1024 == kWaves * kGPW && kTauGPW == 2, "DMA pieces per wave");
 
 // the slot table is re-read at the end of these tiles (used two tiles later); debug MODE 16: at every one
@@ -123,8 +139,7 @@ __device__ __forceinline__ int max3i(int a, int b, int c) { return max(max(a, b)
 // looked at from thr − e2 on.  drop_o: the best A this lane looked at and did not keep.
 // Production: the 16 pass tests make a bit mask first (fold_mask); the list (L) lives in registers for
 // the whole scan, and each lane inserts its passing values one per trip (fold_trip: KL independent
-// compares, no memory); fold_end tightens the own bound and publishes the list's best.  The kernel runs
-// the trips deferred, one per k-step of the next tile, under that tile's MFMAs (DEFER below).  The
+// compares, no memory); fold_end tightens the own bound and publishes the list's best.  The
 // serial LDS insert (one dependent LDS round trip per shifted entry) is debug MODE 1024: a wave in this
 // slow path holds the whole workgroup at the next stage barrier.
 // The pass mask: bit r set = value r is live and reaches thr − e2; pub = the tile's best reaches it (the
@@ -250,8 +265,7 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
 // slow path compiled in but never taken (wrong results; separates its cost from the code's presence),
 // 1024 = the slow path's serial LDS list insert instead of the register-resident list, 16 = the slot
 // table re-read at every one of the first 16 tiles, 2048 = issue priority for a wave in the slow path,
-// 16384 = the slow path deferred: its pass mask at the tile's epilogue, its list inserts one per
-// k-step of the next tile (under that tile's MFMAs), the own bound and slot update at its last k-step.
+// 32768 = the ring without stage barriers (DEC below).
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
@@ -292,6 +306,9 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   uint64_t* const Ls = (uint64_t*)(lds + kListOff) + (w * KL) * 64 + lane;  // debug MODE 1024's list
 #pragma unroll
   for (int i = 0; i < KL; ++i) Ls[i * 64] = 0ull;
+  uint32_t* const ready = (uint32_t*)(lds + ctr_off<KL, RING>());  // MODE 32768: [RING] pieces landed
+  uint32_t* const done = ready + 16;                                  // [RING] waves done reading
+  if (tid < 32) ready[tid] = 0u;  // (the same zeros as the list init above)
   uint64_t Lr[KL];  // production: the lane's list lives in registers for the whole scan
 #pragma unroll
   for (int i = 0; i < KL; ++i) Lr[i] = 0ull;
@@ -396,8 +413,16 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   constexpr int PF = (D == 768 && (MODE & 4) == 0) ? 2 : 1;  // d 1024: 16 k-steps per tile, PF 2 would not realign
   constexpr int NF = PF + 1;
   constexpr int KB = KPS - PF;
-  constexpr int AHEAD = RING - 1;
-  constexpr int YNG = (RING - 2) * kGPW;  // ops younger than the next stage
+  // Debug MODE 32768 (DEC): no stage barrier.  A wave waits only for the 8 pieces of its next stage (the
+  // per-slot `ready` counter) and, before a DMA into a slot, for every wave to be done reading the
+  // slot's previous stage (`done`); LAG free slots let a wave that is in the slow path fall up to LAG
+  // stages behind the others without stalling them.  Pieces go out AHEAD = RING - 1 - LAG stages early.
+  constexpr bool DEC = (MODE & 32768) != 0 && (MODE & 8) == 0;
+  constexpr int LAG = DEC ? 3 : 0;
+  constexpr int AHEAD = RING - 1 - LAG;
+  constexpr int RA = AHEAD + 1;           // the counted-wait arithmetic below is in stages in flight
+  static_assert(AHEAD >= 3, "at least three stages in flight");
+  constexpr int YNG = (RA - 2) * kGPW;  // ops younger than the next stage
   static_assert((NST * KPS) % NF == 0, "fragment rotation must realign every tile");
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // resident queries landed before the counted stream
@@ -409,6 +434,8 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   // 0 .. AHEAD - 1 (with piece 0's own record after it)
   constexpr int NM0 = (AHEAD - 1) / NST + 1;
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(YNG + NM0) : "memory");
+  if constexpr (DEC)
+    if (lane == 0) lds_arrive(&ready[0]);  // stage 0's first use of slot 0 counts like every other
   asm volatile("s_barrier" ::: "memory");
 
   Frag fr[NF];
@@ -418,16 +445,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   // first k-step of MFMAs (production), so its VALU / LDS work overlaps the matrix cores instead of
   // waiting for the MFMA pipeline to drain at every tile end (debug MODE 128: epilogue in place).
   v4i32 accA[4], accB[4];  // [rb * 2 + qb]
-  // The deferred slow path (DEFER): the pass mask of a tile that entered it, the tile's scale and row
-  // base, and whether the lane publishes; the inserts run one per k-step of the next tile, while the
-  // tile's accumulators stay untouched (the next tile accumulates into the other set), and the whole
-  // fold completes at the next tile's last k-step, before any later epilogue reads the bound.
-  constexpr bool DEFER = (MODE & 16384) != 0 && (MODE & (128 | 1024)) == 0;
-  uint32_t pm_p = 0u;
-  float st_p = 0.f;
-  int rb_p = 0;
-  bool pub_p = false, pend = false;
-  auto epilogue = [&](const int it, v4i32(&acc4)[4], const bool defer) {
+  auto epilogue = [&](const int it, v4i32(&acc4)[4]) {
     const int tile = range + it * nblk;
     // Fast path: the max D of each of the lane's two queries, scaled by the tile's scale, against the
     // query's bound (qb 0 values in acc4[0], acc4[2]; qb 1 in acc4[1], acc4[3]).  Only when some lane of the wave
@@ -468,14 +486,6 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
             acc4[2 * rb][i] = (int)r[0];
             acc4[2 * rb + 1][i] = (int)r[1];
           }
-        if (DEFER && defer) {
-          pm_p = fold_mask(acc4, st, lw >> (8 * half), thr, e2, pub_p);
-          st_p = st;
-          rb_p = tile * kTM + 8 * half;
-          pend = true;
-          if constexpr ((MODE & 2048) != 0) __builtin_amdgcn_s_setprio(0);
-          return;
-        }
         fold_screen<KL, (MODE & 1024) == 0>(acc4, st, lw >> (8 * half), Ls, Lr, thr, e2, drop, tile * kTM + 8 * half,
                                             tau_rsrc, slot_voff);
         set_bounds();
@@ -496,11 +506,11 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
     auto nmeta = [&](int s) {
       int c = 0;
 #pragma unroll
-      for (int j = 1; j <= RING - 1; ++j) c += (s + j) % NST == 0;
+      for (int j = 1; j <= RA - 1; ++j) c += (s + j) % NST == 0;
       return c;
     };
     auto young = [&](int s) {
-      const int dmax = (RING - 3 + NST - s) / NST;
+      const int dmax = (RA - 3 + NST - s) / NST;
       bool y = false;
 #pragma unroll
       for (int d = 1; d <= dmax; ++d) y = y || (it >= d && tau_refresh_tile<MODE>(it - d));
@@ -513,13 +523,18 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
 #pragma unroll
       for (int kk = 0; kk < KPS; ++kk) {
         if constexpr ((MODE & 8) == 0)
-          if (kk == 0) issue_piece(g + RING - 1, (g + RING - 1) % RING);
+          if (kk == 0) {
+            const int h = g + AHEAD;
+            if constexpr (DEC)  // the slot's previous stage h - RING read by all 8 waves
+              if (h >= RING) lds_spin_ge(&done[h % RING], (uint32_t)(8 * (h / RING)));
+            issue_piece(h, h % RING);
+          }
         if (kk == KB) {
           if constexpr ((MODE & 8) == 0) {
-            // younger than stage g+1's piece: stages g+2 .. g+RING-1 (YNG), the metadata records issued
-            // with stages g+1 .. g+RING-1 that start a tile (nmeta(s): s = g mod NST), a refresh
+            // younger than stage g+1's piece: stages g+2 .. g+RA-1 (YNG), the metadata records issued
+            // with stages g+1 .. g+RA-1 that start a tile (nmeta(s): s = g mod NST), a refresh
             const int nm = nmeta(s) + (young(s) ? kTauGPW : 0);  // unrolled: a constant per stage
-            static_assert(kTauGPW == 2 && RING <= 13, "wait table below covers nm <= 6");
+            static_assert(kTauGPW == 2 && RA <= 13, "wait table below covers nm <= 6");
             switch (nm) {
 #define RFX_K10_WAIT(N)                                                                  \
   case N:                                                                                \
@@ -533,9 +548,19 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
           } else {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           }
-          asm volatile("s_barrier" ::: "memory");
-          if constexpr ((MODE & 8) == 0)
+          if constexpr (DEC) {
+            // this wave's piece of stage g+1 landed and its reads of stage g completed (the wait above)
+            if (lane == 0) {
+              lds_arrive(&done[g % RING]);
+              lds_arrive(&ready[(g + 1) % RING]);
+            }
             if (s == NST - 1 && tau_refresh_tile<MODE>(it)) issue_tau();
+            if (g + 1 < S) lds_spin_ge(&ready[(g + 1) % RING], (uint32_t)(8 * ((g + 1) / RING + 1)));
+          } else {
+            asm volatile("s_barrier" ::: "memory");
+            if constexpr ((MODE & 8) == 0)
+              if (s == NST - 1 && tau_refresh_tile<MODE>(it)) issue_tau();
+          }
         }
         const int ks = s * KPS + kk;
         fr[(ks + PF) % NF] = kk + PF < KPS ? read_frag(slot, kk + PF) : read_frag((g + 1) % RING, kk + PF - KPS);
@@ -548,22 +573,8 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
           for (int qb = 0; qb < 2; ++qb)
             acc4[2 * rb + qb] = ks == 0 ? mfma_i8(cur.a[rb], bq[2 * ks + qb], v4i32{0, 0, 0, 0})
                                         : mfma_i8(cur.a[rb], bq[2 * ks + qb], acc4[2 * rb + qb]);
-        if constexpr ((MODE & 128) == 0) {
-          if (s == 0 && kk == 0) {
-            if (prev) epilogue(it - 1, accp, true);
-          } else if constexpr (DEFER) {
-            if (pend) {  // (wave-uniform) one insert per lane under this k-step's MFMAs; all of it at the last
-              if (ks < NKS - 1) {
-                if (pm_p) fold_trip<KL>(accp, st_p, rb_p, pm_p, Lr, drop);
-              } else {
-                while (pm_p) fold_trip<KL>(accp, st_p, rb_p, pm_p, Lr, drop);
-                fold_end<KL>(Lr, thr, pub_p, tau_rsrc, slot_voff);
-                set_bounds();
-                pend = false;
-              }
-            }
-          }
-        }
+        if constexpr ((MODE & 128) == 0)
+          if (s == 0 && kk == 0 && prev) epilogue(it - 1, accp);
       }
     }
 
@@ -571,7 +582,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   if constexpr ((MODE & 128) != 0) {
     for (int it = 0; it < nt; ++it) {
       tile_body(it, accA, accB, false);
-      epilogue(it, accA, false);
+      epilogue(it, accA);
     }
   } else {
     int it = 0;
@@ -581,9 +592,9 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
     }
     if (it < nt) {
       tile_body(it, accA, accB, it > 0);
-      epilogue(it, accA, false);
+      epilogue(it, accA);
     } else {
-      epilogue(it - 1, accB, false);
+      epilogue(it - 1, accB);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

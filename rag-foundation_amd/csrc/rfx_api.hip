@@ -1184,6 +1184,42 @@ int rfx_dbg_screen_variant(rfx_index_t h, const void* queries_d, int64_t nq, int
   return RFX_OK;
 }
 
+// Diagnostic: the two-pass search with a kernel-10 variant (quantiser, the variant, select; no gated
+// fallback: *fallback_h says whether it would have run): the variant's answer against production's.
+int rfx_dbg_screen_search(rfx_index_t h, const void* queries_d, int64_t nq, int k, int variant, float* out_s,
+                          int64_t* out_r, void* ws_d, size_t ws_bytes, void* stream, uint32_t* fallback_h) {
+  auto ix = get(h);
+  if (!ix || !fallback_h) return fail(RFX_EINVAL, "unknown index handle / null out");
+  RFX_RLOCK(ix);
+  SearchLayout L;
+  int rc = make_search_layout(*ix, nq, k, L);
+  if (rc) return rc;
+  if (L.kernel != 10 || ws_bytes < L.total) return fail(RFX_EINVAL, "variant needs a two-pass plan and its workspace");
+  hipStream_t st = (hipStream_t)stream;
+  uint8_t* ws = (uint8_t*)ws_d;
+  int8_t* qc = (int8_t*)(ws + L.s_qc);
+  float* qe2 = (float*)(ws + L.s_qe2);
+  uint32_t* stau = (uint32_t*)(ws + L.s_tau);
+  uint32_t* gate = (uint32_t*)(ws + L.s_gate);
+  rfx::launch_screen_queries(queries_d, ix->dtype, ix->dim, nq, L.sp.nq_pad, qc, qe2, ix->sstats, stau, gate, nullptr, st);
+  if (rfx::launch_scan_screen_dbg(L.sp, variant, ix->scodes, ix->smeta, ix->sstats, (int)ix->rows, qc, qe2, (int)nq, stau,
+                                  (float*)(ws + L.s_cs), (int*)(ws + L.s_cr), (uint32_t*)(ws + L.s_drop), st) != 0)
+    return fail(RFX_EUNSUPPORTED, "screen variant %d unsupported", variant);
+  const void* qpad = queries_d;
+  if (nq != L.mp.nq_pad || ((uintptr_t)queries_d & 15)) {
+    qpad = ws + L.q_off;
+    rfx::launch_pad_queries(queries_d, nq, L.mp.nq_pad, ix->dim, 2, (void*)qpad, st);
+  }
+  if (rfx::launch_screen_select((float*)(ws + L.s_cs), (int*)(ws + L.s_cr), (uint32_t*)(ws + L.s_drop), L.sp.n_lists,
+                                L.sp.k_lane, qe2, qpad, ix->data, ix->dim, ix->dtype, nq, k, 0, out_s, out_r, nullptr, gate,
+                                (int*)(ws + L.s_diag), 0, st) != 0)
+    return fail(RFX_EUNSUPPORTED, "screen select k=%d unsupported", k);
+  RFX_HIP(hipGetLastError());
+  RFX_HIP(hipStreamSynchronize(st));
+  RFX_HIP(hipMemcpy(fallback_h, gate, 4, hipMemcpyDeviceToHost));
+  return RFX_OK;
+}
+
 // Diagnostic: after a kernel-10 variant with MODE 32, the slow-path entries it counted (sum over waves).
 int rfx_dbg_screen_counts(rfx_index_t h, int64_t nq, int k, const void* ws_d, uint64_t* out) {
   auto ix = get(h);

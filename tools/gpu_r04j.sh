@@ -1,0 +1,25 @@
+#!/bin/bash
+# round 4: kernel 10 without stage barriers (MODE 32768, per-slot LDS arrival counters): validate against
+# the production answer first (one launch each), then time at the shard and at 10M
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/r04j; mkdir -p $O
+timeout -k 10 120 python -u tools/k10_variants.py --rows 1250000 --variants 800000,1032768 --validate --rounds 0 > $O/k10_dec_validate.txt 2>&1 || { tail -20 $O/k10_dec_validate.txt; exit 1; }
+grep -h "first_launch\|equal" $O/k10_dec_validate.txt
+timeout -k 10 300 python -u tools/k10_variants.py --rows 1250000 --variants 800000,1032768,1232768,800032,1032800 --rounds 8 --burst 100 > $O/k10_shard_dec.txt 2>&1 || { tail -20 $O/k10_shard_dec.txt; exit 1; }
+grep -h "slow_path\|min\|\"[0-9]*\": {" $O/k10_shard_dec.txt
+timeout -k 10 300 python -u tools/k10_variants.py --variants 800000,1032768,1232768 --rounds 6 --validate > $O/k10_10m_dec.txt 2>&1 || { tail -20 $O/k10_10m_dec.txt; exit 1; }
+grep -h "equal\|min\|\"[0-9]*\": {" $O/k10_10m_dec.txt
+O=gpurun_out/r04j; mkdir -p $O
+S='import json,sys; d=json.loads(sys.stdin.readlines()[-1]); print(d["config"]["workload"][:30], d["ms_per_step"], d.get("host_issue_ms_per_step"), d["phases_ms"], d["roofline"]["kernel_ms"])'
+for es in 1 1000; do
+timeout -k 10 300 python -u bench.py --rows 1250000 --force-comm --steps 400 --warmup 20 --no-cpu-baseline --event-stride $es > $O/bench_shard_es$es.log 2>&1 || { tail -30 $O/bench_shard_es$es.log; exit 1; }
+tail -1 $O/bench_shard_es$es.log | python3 -c "$S"
+done
+timeout -k 10 300 python -u bench.py --rows 1250000 --steps 400 --warmup 20 --no-cpu-baseline --event-stride 1000 > $O/bench_shard_nocomm.log 2>&1 || { tail -30 $O/bench_shard_nocomm.log; exit 1; }
+tail -1 $O/bench_shard_nocomm.log | python3 -c "$S"
+timeout -k 10 300 python -u tools/k11_phases.py > $O/k11_phases.json 2>&1 || { tail -20 $O/k11_phases.json; exit 1; }
+cat $O/k11_phases.json | tr -d ' \n'; echo
+timeout -k 10 420 python -u bench.py > $O/bench_cfg3.log 2>&1 || { tail -30 $O/bench_cfg3.log; exit 1; }
+tail -1 $O/bench_cfg3.log | python3 -c "$S"

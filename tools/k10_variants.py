@@ -28,6 +28,7 @@ ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--burst", type=int, default=30)
 ap.add_argument("--variants", default="800000,800001,800009,400000")
 ap.add_argument("--seconds", type=float, default=0.0, help="one variant back to back for this long (power sampling)")
+ap.add_argument("--validate", action="store_true", help="each variant's two-pass answer must equal production's")
 a = ap.parse_args()
 f = _lib.lib.rfx_dbg_screen_variant
 f.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -46,9 +47,34 @@ def launch(v):
     _lib.check(f(ix.handle, _lib.ptr(q), a.nq, a.k, v, _lib.ptr(ws), ws.numel(), st))
 
 
-for v in variants:  # warm + validate every variant launches
+t_first = {}
+for v in variants:  # warm + validate every variant launches (and time one cold launch: a bounded spin gone
+    # wrong would show here as tens of ms before any burst)
+    t0 = time.perf_counter()
     launch(v)
-torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    t_first[v] = round((time.perf_counter() - t0) * 1e3, 3)
+print(json.dumps({"first_launch_ms": t_first}), flush=True)
+if a.validate:  # every variant's two-pass answer (no fallback) against the production search
+    vs = _lib.lib.rfx_dbg_screen_search
+    vs.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
+    vs.restype = ctypes.c_int
+    ref_s, ref_r = ix.search(q, a.k)
+    for v in variants:
+        if (v % 100000) & (1 | 8 | 512):  # timing-only variants (wrong results by design)
+            continue
+        s_ = torch.empty_like(ref_s)
+        r_ = torch.empty_like(ref_r)
+        fb = ctypes.c_uint32()
+        _lib.check(vs(ix.handle, _lib.ptr(q), a.nq, a.k, v, _lib.ptr(s_), _lib.ptr(r_), _lib.ptr(ws), ws.numel(), st,
+                      ctypes.byref(fb)))
+        same = bool(torch.equal(r_, ref_r) and torch.equal(s_, ref_s))
+        print(json.dumps({"variant": v, "equal_to_production": same, "fallback": bool(fb.value)}), flush=True)
+        if not same:
+            sys.exit(f"variant {v} differs from the production search")
+if a.rounds == 0:
+    sys.exit(0)
 if a.seconds > 0:  # steady state of ONE variant (rocm-smi samples power / sclk meanwhile)
     v = variants[0]
     n, t0 = 0, time.time()
