@@ -66,8 +66,11 @@ def parse():
     # oracle check of the last timed step (rank 0, N = 1): every `stride`-th query against
     # oracle.search.topk_blocks over ALL rows (read back after the timed region); 0 = off
     ap.add_argument("--oracle-stride", type=int, default=4)
-    ap.add_argument("--event-stride", type=int, default=1,
-                    help="bracket every Nth timed step with HIP events (kernel_ms = their average)")
+    # An event record is not free on this GPU (~5 us each, measured: profiles/r04k/): the N > 1 step
+    # records 5 per instrumented step, 26 us of a 0.38-ms shard step.  0 = auto: instrument 4 of the
+    # timed steps (every steps/4-th), so the line's ms_per_step carries ~1/5 of that cost
+    ap.add_argument("--event-stride", type=int, default=0,
+                    help="bracket every Nth timed step with HIP events (kernel_ms = their average); 0 = steps // 4")
     # rehearsal of the multi-GPU path on a one-GPU box: gloo transport, every rank on cuda:0,
     # and --check compares the sharded result with a whole-index search on rank 0
     ap.add_argument("--backend", default="rccl", choices=["rccl", "gloo"])
@@ -268,7 +271,8 @@ def main():
 
     for i in range(a.warmup):
         step(i)
-    ev_steps = list(range(0, a.steps, max(1, a.event_stride)))
+    stride = a.event_stride if a.event_stride > 0 else max(1, a.steps // 4)
+    ev_steps = list(range(0, a.steps, stride))
     evs = {i: new_events() for i in ev_steps}
     if world > 1:
         dist.barrier()
@@ -361,7 +365,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": load_pmc_traffic(workload_key, kname),
                      "kernel": kname,
-                     "kernel_ms": round(scan_ms, 4), "event_timed_launches": len(evs),
+                     "kernel_ms": round(scan_ms, 4), "event_timed_launches": len(evs), "event_stride": stride,
                      "alg_bytes_per_launch": alg_bytes},
         "phases_ms": {k_: round(v, 4) for k_, v in phases.items()},
         "host_issue_ms_per_step": round(host_issue / a.steps * 1e3, 4),

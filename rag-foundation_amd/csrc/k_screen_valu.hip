@@ -96,18 +96,50 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   uint32_t* const gate = state + 24;
   RFX_K11_T(0);
 
+  // The int8 row stream (step 2): iteration t scores rows wb + 64 (t >> 4) + 4 (t & 15) + g.  Its first
+  // NB - 1 iterations of loads are issued here, before the query quantiser, so their latency overlaps
+  // it (the rows do not depend on the query).
+  const int wave_g = blockIdx.x * 4 + w;
+  const int wb = (int)min((int64_t)wave_g * rows_per_wave, (int64_t)nrows);
+  const int we = (int)min((int64_t)wb + rows_per_wave, (int64_t)nrows);
+  // force bits 2/4/8/16/32 (RFX_K11_ABLATE, timing only, wrong results): no row stream / no query
+  // quantiser / no last-block work / no re-score and rank / no LB over the records
+  const int T = (force & 2) ? 0 : we > wb ? (we - wb + 15) / 16 * 4 : 0;
+  auto load_row = [&](int t, Codes<D>& v) {
+    const int row = wb + 64 * (t >> 4) + 4 * (t & 15) + g;
+    const int rr = row < we ? row : wb;
+    const int8_t* rp = X8 + (int64_t)rr * D;
+#pragma unroll
+    for (int i = 0; i < C; ++i) v.v[i] = *(const uint4*)(rp + 16 * (j + 16 * i));
+    v.md = tmeta[rr >> 5];  // cache hits after the first row of a tile
+  };
+  // NB row buffers: NB - 1 iterations of loads in flight ahead of the one being scored (one wave per
+  // SIMD has nothing else to hide the latency; 3 in flight measured latency-bound at 2.6 TB/s)
+  constexpr int NB = NQT == 1 ? 8 : 4;
+  Codes<D> buf[NB];
+  // the quantiser's inputs are requested first (the store maxima and this wave's first query), then the
+  // rows: the quantiser then waits for its own loads only, not for the row prefetch behind them
+  constexpr int PL = D / 64;  // query elements per lane
+  const uint32_t st0 = stats[0], st1 = stats[1];
+  float y0[PL];
+#pragma unroll
+  for (int e = 0; e < PL; ++e) y0[e] = w < nq ? qelem<DT>(Q, (int64_t)w * D + lane + 64 * e) : 0.f;
+  if (T > 0) {
+#pragma unroll
+    for (int p = 0; p < NB - 1; ++p) load_row(p, buf[p]);
+  }
+
   // ---- 1. query codes and e2 (every block, identically): wave w quantises queries w, w + 4 ------
   __shared__ __attribute__((aligned(16))) int8_t qc_lds[NQT][D];
   __shared__ float e2_lds[NQT];
   {
-    const double xm = (double)__uint_as_float(stats[0]), em = (double)__uint_as_float(stats[1]);
+    const double xm = (double)__uint_as_float(st0), em = (double)__uint_as_float(st1);
     for (int qi = w; qi < NQT && !(force & 4); qi += 4) {
-      constexpr int PL = D / 64;  // elements per lane
       float y[PL];
       float am = 0.f;
 #pragma unroll
       for (int e = 0; e < PL; ++e) {
-        y[e] = qi < nq ? qelem<DT>(Q, (int64_t)qi * D + lane + 64 * e) : 0.f;
+        y[e] = qi == w ? y0[e] : qi < nq ? qelem<DT>(Q, (int64_t)qi * D + lane + 64 * e) : 0.f;
         am = fmaxf(am, fabsf(y[e]));
       }
 #pragma unroll
@@ -148,13 +180,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
 #pragma unroll
     for (int i = 0; i < C; ++i) qv[qi].v[i] = *(const uint4*)(&qc_lds[qi][16 * (j + 16 * i)]);
 
-  // ---- 2. the int8 row stream: iteration t scores rows wb + 64 (t >> 4) + 4 (t & 15) + g ----------
-  const int wave_g = blockIdx.x * 4 + w;
-  const int wb = (int)min((int64_t)wave_g * rows_per_wave, (int64_t)nrows);
-  const int we = (int)min((int64_t)wb + rows_per_wave, (int64_t)nrows);
-  // force bits 2/4/8/16/32 (RFX_K11_ABLATE, timing only, wrong results): no row stream / no query
-  // quantiser / no last-block work / no re-score and rank / no LB over the records
-  const int T = (force & 2) ? 0 : we > wb ? (we - wb + 15) / 16 * 4 : 0;
+  // ---- 2. the int8 row stream (set up and first loads issued above) -----------------------------
   WaveList<kK> L[NQT];
   float dm[NQT];  // per lane: the best A this wave dropped (rejected at offer time or evicted)
   float cand[NQT];
@@ -164,14 +190,6 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     dm[qi] = -__builtin_inff();
     cand[qi] = __builtin_nanf("");
   }
-  auto load_row = [&](int t, Codes<D>& v) {
-    const int row = wb + 64 * (t >> 4) + 4 * (t & 15) + g;
-    const int rr = row < we ? row : wb;
-    const int8_t* rp = X8 + (int64_t)rr * D;
-#pragma unroll
-    for (int i = 0; i < C; ++i) v.v[i] = *(const uint4*)(rp + 16 * (j + 16 * i));
-    v.md = tmeta[rr >> 5];  // cache hits after the first row of a tile
-  };
   auto score_row = [&](int t, const Codes<D>& v) {
     const int row = wb + 64 * (t >> 4) + 4 * (t & 15) + g;
     const uint4 md = v.md;
@@ -227,14 +245,6 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       l.tr = readlane_i(l.lr, kK - 1);
     }
   };
-  // NB row buffers: NB - 1 iterations of loads in flight ahead of the one being scored (one wave per
-  // SIMD has nothing else to hide the latency; 3 in flight measured latency-bound at 2.6 TB/s)
-  constexpr int NB = NQT == 1 ? 8 : 4;
-  Codes<D> buf[NB];
-  if (T > 0) {
-#pragma unroll
-    for (int p = 0; p < NB - 1; ++p) load_row(p, buf[p]);
-  }
   for (int t = 0; t < T; t += NB) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -255,14 +265,16 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
 
   RFX_K11_T(2);
   // ---- 3. block record per query: the 15 best A of the block (rows), and its drop bound ----------
-  __shared__ float ms[4][NQT][kK];
-  __shared__ int mr[4][NQT][kK];
+  // The four wave lists (sorted, best first, empty entries at the tail) as rank keys (orderable A << 32
+  // | ~row; 0 = empty); the merging wave holds one of the 64 entries per lane and counts the entries
+  // better than its own — a one-compare-per-entry rank, no serial insert loop.
+  __shared__ uint64_t mk[NQT][4 * kK];
   __shared__ float wdm[4][NQT];
 #pragma unroll
   for (int qi = 0; qi < NQT; ++qi) {
     if (lane < kK) {
-      ms[w][qi][lane] = L[qi].ls;
-      mr[w][qi][lane] = L[qi].lr;
+      const bool v = L[qi].lr != kEmptyRow;
+      mk[qi][w * kK + lane] = v ? ((uint64_t)ord_f32(L[qi].ls) << 32) | (uint32_t)(~(uint32_t)L[qi].lr) : 0ull;
     }
     float d = dm[qi];
 #pragma unroll
@@ -271,31 +283,32 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   }
   __syncthreads();
   for (int qi = w; qi < nq; qi += 4) {
-    WaveList<kK> M;
-    M.init();
-#pragma unroll
-    for (int src = 0; src < 4; ++src) {
-      const bool v = lane < kK && mr[src][qi][lane] != kEmptyRow;
-      M.offer(v ? ms[src][qi][lane] : -__builtin_inff(), v ? mr[src][qi][lane] : kEmptyRow, v);
-    }
-    // dropped: the waves' drops, wave-list entries the block list does not hold (strictly worse
-    // than its 16th), and the 16th itself (entry 15 of the record carries the drop bound instead)
+    const uint64_t mine = mk[qi][lane];
+    int rank = 0;
+#pragma unroll 16
+    for (int i = 0; i < 4 * kK; ++i) rank += mk[qi][i] > mine ? 1 : 0;
+    const bool v = mine != 0ull;
+    const float ms_ = unord_f32((uint32_t)(mine >> 32));
+    // dropped: the waves' drops and every entry from the 16th on (the record keeps 15; entry 15 carries
+    // the drop bound instead)
     float d = fmaxf(fmaxf(wdm[0][qi], wdm[1][qi]), fmaxf(wdm[2][qi], wdm[3][qi]));
-#pragma unroll
-    for (int src = 0; src < 4; ++src) {
-      const bool v = lane < kK && mr[src][qi][lane] != kEmptyRow;
-      const float sv = v ? ms[src][qi][lane] : -__builtin_inff();
-      if (v && better(M.ts, M.tr, sv, mr[src][qi][lane])) d = fmaxf(d, sv);
-    }
-    if (lane == kK - 1 && M.lr != kEmptyRow) d = fmaxf(d, M.ls);
+    if (v && rank >= kK - 1) d = fmaxf(d, ms_);
 #pragma unroll
     for (int off = 32; off; off >>= 1) d = fmaxf(d, __shfl_xor(d, off));
-    if (lane < kK) {
-      const int64_t o = ((int64_t)qi * n_lists + blockIdx.x) * kK + lane;
-      const bool rec = lane < kK - 1;
-      __hip_atomic_store((uint32_t*)cand_s + o, __float_as_uint(rec ? M.ls : d), __ATOMIC_RELAXED,
+    const int nv = (int)__popcll(__ballot(v));
+    const int64_t o0 = ((int64_t)qi * n_lists + blockIdx.x) * kK;
+    if (v && rank < kK - 1) {
+      __hip_atomic_store((uint32_t*)cand_s + o0 + rank, __float_as_uint(ms_), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(cand_r + o0 + rank, (int)(~(uint32_t)mine), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane >= nv && lane < kK - 1) {  // empty tail of the record
+      __hip_atomic_store((uint32_t*)cand_s + o0 + lane, __float_as_uint(-__builtin_inff()), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(cand_r + o, rec ? M.lr : kDropRow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(cand_r + o0 + lane, kEmptyRow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == kK - 1) {
+      __hip_atomic_store((uint32_t*)cand_s + o0 + lane, __float_as_uint(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(cand_r + o0 + lane, kDropRow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 
@@ -390,6 +403,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
         const uint32_t mine = hk[tid + 256 * u];
         if (mine) {
           int cnt = 0;
+#pragma unroll 8
           for (int i = 0; i < (m + 3) / 4; ++i) {
             const uint4 v = hk4[i];
             cnt += (v.x >= mine) + (v.y >= mine) + (v.z >= mine) + (v.w >= mine);
@@ -410,6 +424,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     }
     __syncthreads();
     if (qi == 0) RFX_K11_L(2);
+#pragma unroll 4
     for (int i = tid; i < n; i += 256) {
       const int r = br[i];
       if (r != kEmptyRow && r != kDropRow && bs[i] >= cut) {
@@ -423,32 +438,41 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     if (qi == 0) RFX_K11_L(3);
     if (!fail && !(force & 16)) {
       const int ns = n_sv;
-      // exact re-score: 8 lanes per survivor, 32 survivors per round, every row's loads in flight
-      // (a round costs about one memory latency: config 2 has ~2 rounds)
+      // exact re-score: 16 lanes per survivor (16-B chunks gl + 16 u of the row), UR survivors per group
+      // in flight, 32 per round (config 2: ~30 survivors, one round = one memory latency); the query's
+      // chunks are loaded once per query, not per survivor
       constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
       constexpr int EPV = 16 / ESZ;
-      constexpr int VPL = D * ESZ / 128;
-      const int grp = tid >> 3, gl = tid & 7;
-      for (int e0 = 0; e0 < ns; e0 += 32) {
-        const int e = e0 + grp;
-        double acc = 0.0;
-        if (e < ns) {
-          const int r = br[sv[e]];
-          uint4 xv[VPL], yv[VPL];
+      constexpr int VPL = D * ESZ / 256;
+      constexpr int UR = 2;
+      const int grp = tid >> 4, gl = tid & 15;
+      uint4 yv[VPL];
 #pragma unroll
-          for (int u = 0; u < VPL; ++u) {
-            xv[u] = *(const uint4*)((const uint8_t*)X + (int64_t)r * D * ESZ + (int64_t)(gl + 8 * u) * 16);
-            yv[u] = *(const uint4*)((const uint8_t*)Q + (int64_t)qi * D * ESZ + (int64_t)(gl + 8 * u) * 16);
-          }
+      for (int u = 0; u < VPL; ++u)
+        yv[u] = *(const uint4*)((const uint8_t*)Q + (int64_t)qi * D * ESZ + (int64_t)(gl + 16 * u) * 16);
+      for (int e0 = 0; e0 < ns; e0 += 16 * UR) {
+        uint4 xv[UR][VPL];
+#pragma unroll
+        for (int ur = 0; ur < UR; ++ur) {
+          const int e = e0 + grp + 16 * ur;
+          const int r = br[sv[e < ns ? e : 0]];
+#pragma unroll
+          for (int u = 0; u < VPL; ++u)
+            xv[ur][u] = *(const uint4*)((const uint8_t*)X + (int64_t)r * D * ESZ + (int64_t)(gl + 16 * u) * 16);
+        }
+#pragma unroll
+        for (int ur = 0; ur < UR; ++ur) {
+          const int e = e0 + grp + 16 * ur;
+          double acc = 0.0;
 #pragma unroll
           for (int u = 0; u < VPL; ++u)
 #pragma unroll
-            for (int ee = 0; ee < EPV; ++ee) acc += (double)elem<DT>(xv[u], ee) * (double)elem<DT>(yv[u], ee);
-        }
+            for (int ee = 0; ee < EPV; ++ee) acc += (double)elem<DT>(xv[ur][u], ee) * (double)elem<DT>(yv[u], ee);
 #pragma unroll
-        for (int off = 4; off; off >>= 1) acc += __shfl_xor(acc, off);  // within the 8-lane group
-        if (gl == 0 && e < ns)
-          skey[e] = ((uint64_t)ord_f32((float)acc) << 32) | (uint32_t)(~(uint32_t)br[sv[e]]);
+          for (int off = 8; off; off >>= 1) acc += __shfl_xor(acc, off);  // within the 16-lane group
+          if (gl == 0 && e < ns)
+            skey[e] = ((uint64_t)ord_f32((float)acc) << 32) | (uint32_t)(~(uint32_t)br[sv[e]]);
+        }
       }
       __syncthreads();
       // top-k of the survivors by (exact score desc, row asc): each survivor counts those ahead of it

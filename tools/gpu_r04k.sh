@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4: event overhead of the N > 1 step (events every step vs once), host issue time, kernel 11
+# round 4 (r04k): event overhead of the N > 1 step (events every step vs once), host issue time, kernel 11
 # phases at config 2, the config-3 default step
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
