@@ -82,6 +82,11 @@ def parse():
     # RCCL exchange of the N > 1 step: "gather" (default) = every rank's records to rank 0, where the
     # answer is assembled (grouped send / recv, one hop); "allgather" = every rank gets all records
     ap.add_argument("--exchange", default="gather", choices=["gather", "allgather"])
+    # the N > 1 step over RCCL with the two-pass plan: batch i's select, fallback, exchange and gathered
+    # merge run on stream B (CU 0 of every XCD) while batch i + 1's screen runs on stream A (the other
+    # CUs, kernel 10 on 248 workgroups); double-buffered workspaces.  auto = on for that step
+    ap.add_argument("--pipeline", default="auto", choices=["auto", "on", "off"])
+    ap.add_argument("--reserve-cus", type=int, default=8, help="--pipeline: CUs (bits 0..n-1 of the CU mask) for stream B")
     return ap.parse_args()
 
 
@@ -230,7 +235,74 @@ def main():
             x.record(stream)
         return e
 
+    # ---- the pipelined N > 1 step (see --pipeline) ------------------------------------------------------
+    pipe = multi and comm is not None and kern == 10 and a.pipeline != "off"
+    pipe_cfg = None
+    if pipe:
+        ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+        res = max(1, min(a.reserve_cus, ncu - 1))
+        nw = -(-ncu // 32)
+        # CU mask bit i = CU i; the driver deals a multi-XCD part's mask bits out to the XCDs in turn, so
+        # bits 0 .. 7 are one CU of each of the 8 XCDs (checked on the box: kernel 10 on the other 248 CUs
+        # runs at 256/248 of its full-chip time, profiles/r04*/)
+        ma = (ctypes.c_uint32 * nw)(*[0xffffffff] * nw)
+        mb = (ctypes.c_uint32 * nw)(*[0] * nw)
+        for b in range(res):
+            ma[b // 32] &= ~(1 << (b % 32)) & 0xffffffff
+            mb[b // 32] |= 1 << (b % 32)
+        pa, pb = ctypes.c_void_p(), ctypes.c_void_p()
+        check(lib.rfx_stream_create_cu_mask(local, ma, nw, ctypes.byref(pa)))
+        check(lib.rfx_stream_create_cu_mask(local, mb, nw, ctypes.byref(pb)))
+        sA = torch.cuda.ExternalStream(pa.value, device=dev)
+        sB = torch.cuda.ExternalStream(pb.value, device=dev)
+        scan_blocks = ncu - res
+        wsP = [ws, torch.empty_like(ws)]
+        recP = [rec, torch.empty_like(rec)]
+        gathP = [gathered, torch.empty_like(gathered)]
+        mgP = [(mg_s, mg_r), (torch.empty_like(mg_s), torch.empty_like(mg_r))]
+        evK = [torch.cuda.Event(), torch.cuda.Event()]
+        evD = [torch.cuda.Event(), torch.cuda.Event()]
+        pipe_cfg = {"streams": 2, "scan_cus": ncu - res, "post_cus": res, "scan_blocks": scan_blocks,
+                    "note": "batch i's select + gated fallback + exchange + gathered merge (stream B) overlap batch "
+                            "i+1's quantiser + kernel 10 (stream A); double-buffered workspaces"}
+
+    def pstep(i, ev=None):
+        sl = i % 2
+        h = ixs[i % copies].handle
+        if i >= 2:
+            sA.wait_event(evD[sl])  # batch i - 2 done with workspace / records slot sl
+        if ev is not None:
+            ev[0].record(sA)
+        check(lib.rfx_search_staged(h, ptr(q), a.nq, a.k, None, 0, r0, None, None, ptr(recP[sl]), ptr(wsP[sl]),
+                                    wsP[sl].numel(), 1, scan_blocks, ctypes.c_void_p(sA.cuda_stream)))
+        if ev is not None:
+            ev[1].record(sA)
+        evK[sl].record(sA)
+        sB.wait_event(evK[sl])
+        check(lib.rfx_search_staged(h, ptr(q), a.nq, a.k, None, 0, r0, None, None, ptr(recP[sl]), ptr(wsP[sl]),
+                                    wsP[sl].numel(), 2, scan_blocks, ctypes.c_void_p(sB.cuda_stream)))
+        if ev is not None:
+            ev[2].record(sB)
+        if a.exchange == "gather":
+            comm.gather_records([recP[sl]], [gathP[sl] if rank == 0 else None], [sB], root=0)
+        else:
+            comm.allgather_records([recP[sl]], [gathP[sl]], [sB])
+        if ev is not None:
+            ev[3].record(sB)
+        res_ = None
+        if a.exchange != "gather" or rank == 0:
+            ms_, mr_ = mgP[sl]
+            check(lib.rfx_merge_gathered(ptr(gathP[sl]), world, a.nq, a.k, ptr(ms_), ptr(mr_),
+                                         ctypes.c_void_p(sB.cuda_stream)))
+            res_ = (ms_, mr_)
+        if ev is not None:
+            ev[4].record(sB)
+        evD[sl].record(sB)
+        return res_
+
     def step(i, ev=None):
+        if pipe:
+            return pstep(i, ev)
         h = ixs[i % copies].handle
         e0 = ctypes.c_void_p(ev[0].cuda_event) if ev is not None else None
         e1 = ctypes.c_void_p(ev[1].cuda_event) if ev is not None else None
@@ -359,7 +431,8 @@ def main():
                                 if comm is not None else
                                 exchange_note if exchange_note else
                                 "host (gloo) rehearsal" if world > 1 else "none (one shard)"),
-                   "scan_kernel": SCAN_NAMES[kern] + (f" ({scan_note})" if scan_note else "")},
+                   "scan_kernel": SCAN_NAMES[kern] + (f" ({scan_note})" if scan_note else ""),
+                   "pipeline": pipe_cfg},
         "achieved_hbm_gbps_per_gpu": round(achieved, 1),
         "build_id": _lib.BUILD_ID,
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",

@@ -220,6 +220,20 @@ int rfx_search_records(rfx_index_t h, const void* queries_d, int64_t nq, int k, 
  * out_records_d is not NULL, records; ev_scan_begin / ev_scan_end (hipEvent_t, may be NULL) are
  * recorded on the stream right before and after the scan kernel (the int8 screen of the two-pass
  * scan, the exact scan, or the one-launch VALU search as a whole). */
+/* The search in two stages, for callers that overlap consecutive batches on two streams (the
+ * multi-GPU step: the select / fallback / exchange of batch i run beside the screen of batch i + 1):
+ * stages bit 1 = the query quantiser + the scan (kernel 10 for a two-pass plan; the whole search for any
+ * other plan), bit 2 = the select + the gated exact fallback (two-pass plans; nothing otherwise).  Both
+ * calls of one batch pass the same arguments; the caller orders stage 2 after stage 1 (an event).
+ * scan_blocks (0 = the plan's 256): the screen's workgroups, so a batch can leave CUs free for the other
+ * stream (rfx_stream_create_cu_mask); the workspace of rfx_search_workspace_bytes covers any value. */
+int rfx_search_staged(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d,
+                      int64_t mask_words, int64_t row_offset, float* out_scores_d, int64_t* out_rows_d,
+                      void* out_records_d, void* ws_d, size_t ws_bytes, int stages, int scan_blocks, void* stream);
+/* A stream restricted to the CUs whose bits are set (hipExtStreamCreateWithCUMask; n_words 32-bit words,
+ * bit i = CU i), on `device`; rfx_stream_destroy releases it. */
+int rfx_stream_create_cu_mask(int device, const uint32_t* cu_mask, int n_words, void** out_stream);
+int rfx_stream_destroy(void* stream);
 int rfx_search_timed(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d,
                      int64_t mask_words, int64_t row_offset, float* out_scores_d, int64_t* out_rows_d,
                      void* out_records_d, void* ws_d, size_t ws_bytes, void* stream, void* ev_scan_begin,

@@ -432,7 +432,7 @@ void launch_screen_quantize(const void* X, int D, int dtype, int64_t tile0, int6
 #undef RFX_SQ
 }
 
-MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k) {
+MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k, int max_blocks) {
   MfmaPlan p{};
   p.ok = screen_supported(D, dtype) && nrows > 0;
   p.k_lane = k <= 4 ? 4 : (k <= 10 ? 10 : -1);
@@ -442,7 +442,7 @@ MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k) {
   p.nq_pad = (int64_t)p.q_blocks * k10::kQG;
   if (p.q_blocks < 1 || p.q_blocks > 256) p.ok = false;
   const int64_t ntiles = std::max<int64_t>((nrows + k10::kTM - 1) / k10::kTM, 1);
-  int64_t ranges = std::max<int64_t>(256 / std::max(p.q_blocks, 1), 1);
+  int64_t ranges = std::max<int64_t>((max_blocks > 0 ? max_blocks : 256) / std::max(p.q_blocks, 1), 1);
   ranges = std::min<int64_t>(ranges, ntiles);
   p.blocks = (int)ranges;
   p.tiles_per_block = (int)((ntiles + ranges - 1) / ranges);

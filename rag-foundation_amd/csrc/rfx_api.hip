@@ -276,13 +276,15 @@ struct SearchLayout {
 
 size_t align_up(size_t x) { return (x + 255) / 256 * 256; }
 
-int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L, bool search = false);
+int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L, bool search = false, int scan_blocks = 0);
 
 // The search plan: the exact layout, extended by the two-pass scan's regions when the index holds an
 // int8 copy and the exact plan is the config-3 / config-4 kernel (6 / 8) it falls back to.
-int make_search_layout(const Index& ix, int64_t nq, int k, SearchLayout& L) { return make_layout(ix, nq, k, L, true); }
+int make_search_layout(const Index& ix, int64_t nq, int k, SearchLayout& L, int scan_blocks = 0) {
+  return make_layout(ix, nq, k, L, true, scan_blocks);
+}
 
-int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L, bool search) {
+int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L, bool search, int scan_blocks) {
   if (k < 1 || k > 64) return fail(RFX_EINVAL, "k=%d out of range [1, 64]", k);
   if (nq < 0) return fail(RFX_EINVAL, "nq < 0");
   if (ix.rows >= (int64_t)INT32_MAX) return fail(RFX_EUNSUPPORTED, "shard exceeds 2^31-1 rows");
@@ -363,7 +365,7 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L, bool search
   L.total = L.cr_off + align_up((size_t)nq * L.n_cand * 4);
   L.fbk = 0;
   if (search && ix.screen && ix.rows > 0 && (L.kernel == 6 || L.kernel == 8)) {
-    L.sp = rfx::plan_scan_screen(ix.rows, ix.dim, ix.dtype, nq, k);
+    L.sp = rfx::plan_scan_screen(ix.rows, ix.dim, ix.dtype, nq, k, scan_blocks);
     if (L.sp.ok) {
       L.fbk = L.kernel;
       L.kernel = 10;
@@ -485,7 +487,7 @@ int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq,
 // Writes (out_s, out_r) or, with out_rec, the {score, pad, row + row_offset} records.
 int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t nq, int k, const uint32_t* mask,
                   int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec, uint8_t* ws, hipStream_t st,
-                  void* ev0 = nullptr, void* ev1 = nullptr) {
+                  void* ev0 = nullptr, void* ev1 = nullptr, int stages = 3) {
   if (nq == 0) return RFX_OK;
   int8_t* qc = (int8_t*)(ws + L.s_qc);
   float* qe2 = (float*)(ws + L.s_qe2);
@@ -499,13 +501,19 @@ int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t
   // the fallback's threshold table is zeroed by the query quantiser when it covers the fallback's
   // padded batch (kernel 10 pads to 256 queries, kernels 6 / 8 to 256 / 128): no memset launch
   const bool ftau = L.mp.nq_pad <= L.sp.nq_pad;
-  rfx::launch_screen_queries(queries, ix.dtype, ix.dim, nq, L.sp.nq_pad, qc, qe2, ix.sstats, stau, gate,
-                             ftau ? tau : nullptr, st);
-  if (ev0) RFX_HIP(hipEventRecord((hipEvent_t)ev0, st));
-  if (rfx::launch_scan_screen(L.sp, ix.scodes, ix.smeta, ix.sstats, (int)ix.rows, ix.dim, qc, qe2, (int)nq, stau, scs,
-                              scr, drops, st, mask) != 0)
-    return fail(RFX_EUNSUPPORTED, "screen scan launch rejected");
-  if (ev1) RFX_HIP(hipEventRecord((hipEvent_t)ev1, st));
+  if (stages & 1) {
+    rfx::launch_screen_queries(queries, ix.dtype, ix.dim, nq, L.sp.nq_pad, qc, qe2, ix.sstats, stau, gate,
+                               ftau ? tau : nullptr, st);
+    if (ev0) RFX_HIP(hipEventRecord((hipEvent_t)ev0, st));
+    if (rfx::launch_scan_screen(L.sp, ix.scodes, ix.smeta, ix.sstats, (int)ix.rows, ix.dim, qc, qe2, (int)nq, stau, scs,
+                                scr, drops, st, mask) != 0)
+      return fail(RFX_EUNSUPPORTED, "screen scan launch rejected");
+    if (ev1) RFX_HIP(hipEventRecord((hipEvent_t)ev1, st));
+  }
+  if (!(stages & 2)) {
+    RFX_HIP(hipGetLastError());
+    return RFX_OK;
+  }
   // the select and the gated exact pass read the queries with 16-B loads: an unaligned batch (or one
   // that is not a whole number of the fallback's query groups) is copied once into the workspace
   const void* qpad = queries;
@@ -1280,12 +1288,14 @@ namespace {
 // one-launch VALU search as a whole): the benchmark's per-kernel timing.
 int search_impl(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d, int64_t mask_words,
                 int64_t row_offset, float* out_scores_d, int64_t* out_rows_d, void* out_rec, void* ws_d, size_t ws_bytes,
-                void* stream, void* ev0, void* ev1) {
+                void* stream, void* ev0, void* ev1, int stages = 3, int scan_blocks = 0) {
   auto ix = get(h);
   if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  if (stages < 1 || stages > 3) return fail(RFX_EINVAL, "stages %d: bit 1 scan, bit 2 select", stages);
+  if (scan_blocks < 0 || scan_blocks > 256) return fail(RFX_EINVAL, "scan_blocks %d out of [0, 256]", scan_blocks);
   RFX_RLOCK(ix);
   SearchLayout L;
-  int rc = make_search_layout(*ix, nq, k, L);
+  int rc = make_search_layout(*ix, nq, k, L, scan_blocks);
   if (rc) return rc;
   if (ws_bytes < L.total || (L.total && !ws_d)) return fail(RFX_EINVAL, "workspace too small (%zu < %zu)", ws_bytes, L.total);
   if (nq > 0 && (!queries_d || (!out_rec && (!out_scores_d || !out_rows_d)))) return fail(RFX_EINVAL, "null queries / outputs");
@@ -1301,7 +1311,8 @@ int search_impl(rfx_index_t h, const void* queries_d, int64_t nq, int k, const u
   };
   if (L.kernel == 10)
     return screen_search(*ix, L, queries_d, nq, k, row_mask_d, row_offset, out_scores_d, out_rows_d, out_rec, ws, st,
-                         ev0, ev1);
+                         ev0, ev1, stages);
+  if (!(stages & 1)) return RFX_OK;  // another plan: the whole search is stage 1
   if (nq == 0) return RFX_OK;
   float* cs = (float*)(ws + L.cs_off);
   int32_t* cr = (int32_t*)(ws + L.cr_off);
@@ -1394,6 +1405,28 @@ int rfx_search_timed(rfx_index_t h, const void* queries_d, int64_t nq, int k, co
                      void* ev_scan_end) {
   return search_impl(h, queries_d, nq, k, row_mask_d, mask_words, row_offset, out_scores_d, out_rows_d, out_records_d,
                      ws_d, ws_bytes, stream, ev_scan_begin, ev_scan_end);
+}
+
+int rfx_search_staged(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d,
+                      int64_t mask_words, int64_t row_offset, float* out_scores_d, int64_t* out_rows_d,
+                      void* out_records_d, void* ws_d, size_t ws_bytes, int stages, int scan_blocks, void* stream) {
+  return search_impl(h, queries_d, nq, k, row_mask_d, mask_words, row_offset, out_scores_d, out_rows_d, out_records_d,
+                     ws_d, ws_bytes, stream, nullptr, nullptr, stages, scan_blocks);
+}
+
+int rfx_stream_create_cu_mask(int device, const uint32_t* cu_mask, int n_words, void** out_stream) {
+  if (!cu_mask || n_words < 1 || !out_stream) return fail(RFX_EINVAL, "null mask / out or n_words < 1");
+  RFX_HIP(hipSetDevice(device));
+  hipStream_t s = nullptr;
+  RFX_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)n_words * 32u, cu_mask));
+  *out_stream = (void*)s;
+  return RFX_OK;
+}
+
+int rfx_stream_destroy(void* stream) {
+  if (!stream) return RFX_OK;
+  RFX_HIP(hipStreamDestroy((hipStream_t)stream));
+  return RFX_OK;
 }
 
 int rfx_search_plan(rfx_index_t h, int64_t nq, int k, int* out_kernel) {

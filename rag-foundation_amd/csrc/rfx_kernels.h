@@ -143,7 +143,7 @@ bool screen_supported(int D, int dtype);
 // tmeta: per tile 16 B {f32 scale, u32 live word, 0, 0}
 void launch_screen_quantize(const void* X, int D, int dtype, int64_t tile0, int64_t ntiles, const int64_t* tiles_d,
                             int8_t* codes, void* tmeta, uint32_t* stats, hipStream_t st);
-MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k);
+MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k, int max_blocks = 0);
 size_t tau_bytes_screen(const MfmaPlan& p);
 // ftau (or null): the gated fallback scan's threshold table ([nq_pad][kFallbackTauW], kernel 6 / 8),
 // zeroed here so the fallback launch needs no memset of its own (tau_zeroed below)
