@@ -84,8 +84,10 @@ def parse():
     ap.add_argument("--exchange", default="gather", choices=["gather", "allgather"])
     # the N > 1 step over RCCL with the two-pass plan: batch i's select, fallback, exchange and gathered
     # merge run on stream B (CU 0 of every XCD) while batch i + 1's screen runs on stream A (the other
-    # CUs, kernel 10 on 248 workgroups); double-buffered workspaces.  auto = on for that step
-    ap.add_argument("--pipeline", default="auto", choices=["auto", "on", "off"])
+    # CUs, kernel 10 on 248 workgroups); double-buffered workspaces.  Off by default: measured slower
+    # (profiles/r04n/: 0.60 against 0.377 ms per shard step — the screen on the masked CUs and the select
+    # on 8 CUs both lose more than the overlap hides)
+    ap.add_argument("--pipeline", default="off", choices=["on", "off"])
     ap.add_argument("--reserve-cus", type=int, default=8, help="--pipeline: CUs (bits 0..n-1 of the CU mask) for stream B")
     return ap.parse_args()
 
@@ -236,7 +238,7 @@ def main():
         return e
 
     # ---- the pipelined N > 1 step (see --pipeline) ------------------------------------------------------
-    pipe = multi and comm is not None and kern == 10 and a.pipeline != "off"
+    pipe = multi and comm is not None and kern == 10 and a.pipeline == "on"
     pipe_cfg = None
     if pipe:
         ncu = torch.cuda.get_device_properties(dev).multi_processor_count

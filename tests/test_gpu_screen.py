@@ -173,3 +173,36 @@ def test_small_and_empty(rindex):
     rows32 = _widen(osynth.synth_rows(21, 0, 7, 768, "bf16"), "bf16")
     s, r = _check(ix, rows32, q, q32, 10)
     assert (r[:, 7:] == -1).all()
+
+
+def test_staged_search_on_two_streams_equals_one_call():
+    """rfx_search_staged: stage 1 (quantiser + kernel 10, on fewer workgroups) on one stream, stage 2
+    (select + gated fallback) on another, ordered by an event, writes the same records as one
+    rfx_search_records call — including a forced fallback, and a VALU plan (stage 1 = the whole search)."""
+    import ctypes
+
+    from rfx._lib import check, lib, ptr
+    from rfx.index import DeviceIndex, synth_rows
+
+    ix = DeviceIndex(768, "bf16", 0)
+    ix.add_synthetic(31, 150_000)
+    ix.enable_screen(1)
+    for nq, mode in ((256, 1), (256, 2), (3, 1)):
+        ix.enable_screen(mode)
+        q = synth_rows(32, 0, nq, 768, "bf16")
+        ref = ix.search_records(q, 10, row_offset=1000)
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        for blocks in (0, 248, 77):
+            ws = torch.empty(ix.workspace_bytes(nq, 10), dtype=torch.uint8, device="cuda")
+            out = torch.full((nq, 10, 2), 7, dtype=torch.int64, device="cuda")
+            ev = torch.cuda.Event()
+            s1.wait_stream(torch.cuda.current_stream())
+            check(lib.rfx_search_staged(ix.handle, ptr(q), nq, 10, None, 0, 1000, None, None, ptr(out), ptr(ws),
+                                        ws.numel(), 1, blocks, ctypes.c_void_p(s1.cuda_stream)))
+            ev.record(s1)
+            s2.wait_event(ev)
+            check(lib.rfx_search_staged(ix.handle, ptr(q), nq, 10, None, 0, 1000, None, None, ptr(out), ptr(ws),
+                                        ws.numel(), 2, blocks, ctypes.c_void_p(s2.cuda_stream)))
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref), (nq, mode, blocks)
+    ix.enable_screen(1)
