@@ -63,8 +63,8 @@ def parse():
     ap.add_argument("--allow-host-exchange", action="store_true",
                     help="N > 1: if RCCL cannot be initialised, exchange through host memory instead of failing")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    # oracle check of the last timed step (rank 0, N = 1): every `stride`-th query against
-    # oracle.search.topk_blocks over ALL rows (read back after the timed region); 0 = off
+    # oracle check of the last timed step (rank 0; at N > 1 the gathered answer): every `stride`-th
+    # query against oracle.search.topk_blocks over ALL rows (after the timed region); 0 = off
     ap.add_argument("--oracle-stride", type=int, default=4)
     # An event record is not free on this GPU (~5 us each, measured: profiles/r04k/): the N > 1 step
     # records 5 per instrumented step, 26 us of a 0.38-ms shard step.  0 = auto: instrument 4 of the
@@ -479,8 +479,16 @@ def main():
             "note": "step_bytes = kernel 10's bytes + select (candidate lists, bf16 queries, survivor rows)"}
 
     check_ok = True
-    if rank == 0 and world == 1 and a.oracle_stride > 0:
-        result["oracle_check"] = oracle_check(ix, q, out, a)
+    if rank == 0 and a.oracle_stride > 0 and out is not None:
+        if multi:
+            # rank 0 holds the gathered answer (global rows) but only its own shard: the oracle reads
+            # every shard's rows from the same counter-based generator the ranks built them from
+            def read(r, n):
+                return synth_rows(a.seed, r, n, a.dim, a.dtype, local)
+        else:
+            read = ix.read
+        result["oracle_check"] = oracle_check(read, a.rows, q, out, a)
+        result["oracle_check"]["answer"] = "gathered merge (rank 0)" if multi else "single shard"
         check_ok = result["oracle_check"]["ok"]
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(ix, q, a)
@@ -496,11 +504,12 @@ def main():
         raise SystemExit("oracle check of the last timed step FAILED (see oracle_check in the JSON line)")
 
 
-def oracle_check(ix, q, out, a):
+def oracle_check(read, n_rows, q, out, a):
     """Checker (not timed): the last timed step's top-k for every a.oracle_stride-th query against
-    the CPU oracle over ALL rows of the corpus, read back from HBM 1M rows at a time and widened
-    exactly to f32 on the host (oracle.search.topk_blocks: f32 screen with a rigorous rounding
-    bound + exact rescoring).  Parity rule: oracle.search.check_topk (1e-5 / 2e-6)."""
+    the CPU oracle over ALL rows of the corpus, read 1M rows at a time (`read(row0, n)`: back from
+    HBM at N = 1; regenerated on rank 0 for the gathered answer of N > 1) and widened exactly to f32
+    on the host (oracle.search.topk_blocks: f32 screen with a rigorous rounding bound + exact
+    rescoring).  Parity rule: oracle.search.check_topk (1e-5 / 2e-6)."""
     import numpy as np
 
     from oracle import search as osearch
@@ -511,19 +520,19 @@ def oracle_check(ix, q, out, a):
     blk = 1 << 20
 
     def blocks():
-        for r0 in range(0, ix.rows, blk):
-            yield r0, ix.read(r0, min(blk, ix.rows - r0)).cpu().float().numpy()
+        for r0 in range(0, n_rows, blk):
+            yield r0, read(r0, min(blk, n_rows - r0)).cpu().float().numpy()
 
     ref_s, ref_r = osearch.topk_blocks(q64, blocks(), a.k)
     got_s, got_r = out[0][sel].cpu().numpy(), out[1][sel].cpu().numpy()
 
     def scores_of(qi, rows):
-        return np.array([ix.read(int(x), 1).cpu().float().numpy()[0].astype(np.float64) @ q64[qi] for x in rows])
+        return np.array([read(int(x), 1).cpu().float().numpy()[0].astype(np.float64) @ q64[qi] for x in rows])
 
     probs = osearch.check_topk(got_s, got_r, ref_s, ref_r, scores_of, tol=1e-5, tie_band=2e-6)
     same = got_r == ref_r
     err = float(np.abs(got_s[same].astype(np.float64) - ref_s[same]).max()) if same.any() else 0.0
-    return {"ok": not probs, "queries": len(sel), "rows": ix.rows, "problems": probs[:3],
+    return {"ok": not probs, "queries": len(sel), "rows": n_rows, "problems": probs[:3],
             "rows_identical_frac": round(float(same.mean()), 6), "max_abs_score_err": err,
             "rule": "oracle.search.check_topk tol 1e-5, tie band 2e-6", "secs": round(time.perf_counter() - t0, 1)}
 

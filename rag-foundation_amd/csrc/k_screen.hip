@@ -181,11 +181,10 @@ __global__ __launch_bounds__(256) void screen_queries_kernel(const uint16_t* __r
       am = fmaxf(am, fabsf(y[m][e]));
     }
   }
-#pragma unroll
-  for (int off = 32; off; off >>= 1) am = fmaxf(am, __shfl_xor(am, off));
+  am = wave_max_f32(am);  // DPP + readlane, no ds_bpermute round trips (rfx_device.h)
   const float s = am > 0.f ? __fdiv_rn(am, 127.f) : 0.f;
   double ey = 0.0;
-  long long cc = 0;
+  int cc = 0;  // <= D 127^2 < 2^31
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
     uint32_t pk = 0u;
@@ -195,15 +194,12 @@ __global__ __launch_bounds__(256) void screen_queries_kernel(const uint16_t* __r
       pk |= (uint32_t)(uint8_t)c << (8 * e);
       const double d = (double)y[m][e] - (double)s * (double)c;
       ey += d * d;
-      cc += (long long)c * c;
+      cc += (int)c * c;
     }
     *(uint32_t*)(Qc + (int64_t)q * D + 256 * m + 4 * lane) = pk;
   }
-#pragma unroll
-  for (int off = 32; off; off >>= 1) {
-    ey += __shfl_xor(ey, off);
-    cc += __shfl_xor(cc, off);
-  }
+  ey = wave_sum_f64(ey);
+  cc = wave_sum_i32(cc);
   if (lane == 0) {
     float e2 = 0.f;
     if (s > 0.f) {
@@ -357,8 +353,7 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
           acc += (double)(widen<DT>(xh) * widen<DT>(yh));
         }
       }
-#pragma unroll
-      for (int off = 8; off; off >>= 1) acc += __shfl_xor(acc, off);  // within the 16-lane group
+      acc = row16_sum_f64(acc);  // within the 16-lane group (DPP; lane 0's sum = the xor butterfly's)
       const int j = j0 + u * NW * 4;
       if (gl == 0 && j < ns) skey[j] = ((uint64_t)ord((float)acc) << 32) | (uint32_t)(~(uint32_t)srow[j]);
     }

@@ -117,13 +117,25 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   // SIMD has nothing else to hide the latency; 3 in flight measured latency-bound at 2.6 TB/s)
   constexpr int NB = NQT == 1 ? 8 : 4;
   Codes<D> buf[NB];
-  // the quantiser's inputs are requested first (the store maxima and this wave's first query), then the
-  // rows: the quantiser then waits for its own loads only, not for the row prefetch behind them
+  // The quantiser's inputs are requested first (the store maxima and this wave's first query, loaded
+  // unconditionally: a load under a wave-uniform condition becomes a branch around it, and the join after
+  // it a vmcnt(0) wait on everything in flight) and its max |y| is reduced before the row prefetch is
+  // issued: that wait covers the query loads only.  The codes and e2 are then computed while the rows
+  // are in flight.
   constexpr int PL = D / 64;  // query elements per lane
   const uint32_t st0 = stats[0], st1 = stats[1];
+  const int wq = w < nq ? w : nq - 1;
+  const float wmf = w < nq ? 1.f : 0.f;  // a multiply, not a select: no branch around the loads
   float y0[PL];
 #pragma unroll
-  for (int e = 0; e < PL; ++e) y0[e] = w < nq ? qelem<DT>(Q, (int64_t)w * D + lane + 64 * e) : 0.f;
+  for (int e = 0; e < PL; ++e) y0[e] = qelem<DT>(Q, (int64_t)wq * D + lane + 64 * e);
+  float am0 = 0.f;
+#pragma unroll
+  for (int e = 0; e < PL; ++e) {
+    y0[e] *= wmf;
+    am0 = fmaxf(am0, fabsf(y0[e]));
+  }
+  am0 = wave_max_f32(am0);
   if (T > 0) {
 #pragma unroll
     for (int p = 0; p < NB - 1; ++p) load_row(p, buf[p]);
@@ -132,44 +144,46 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   // ---- 1. query codes and e2 (every block, identically): wave w quantises queries w, w + 4 ------
   __shared__ __attribute__((aligned(16))) int8_t qc_lds[NQT][D];
   __shared__ float e2_lds[NQT];
-  {
-    const double xm = (double)__uint_as_float(st0), em = (double)__uint_as_float(st1);
-    for (int qi = w; qi < NQT && !(force & 4); qi += 4) {
+  const double xm = (double)__uint_as_float(st0), em = (double)__uint_as_float(st1);
+  // codes c = rint(y / s) clamped to +-127 (s = max|y| / 127), and e2 from the codes themselves; no
+  // branches (s = 0: codes 0, e2 0)
+  auto quant = [&](int qi, const float* y, float am) {
+    const float s = am > 0.f ? __fdiv_rn(am, 127.f) : 0.f;
+    const float sd = s > 0.f ? s : 1.f;
+    double ey = 0.0;
+    int cc = 0;  // <= 64 PL 127^2 < 2^31
+#pragma unroll
+    for (int e = 0; e < PL; ++e) {
+      int c = (int)fminf(fmaxf(rintf(__fdiv_rn(y[e], sd)), -127.f), 127.f);
+      c = s > 0.f ? c : 0;
+      qc_lds[qi][lane + 64 * e] = (int8_t)c;
+      const double dd = (double)y[e] - (double)s * (double)c;
+      ey += dd * dd;
+      cc += c * c;
+    }
+    ey = wave_sum_f64(ey);
+    cc = wave_sum_i32(cc);
+    if (lane == 0) {
+      const double yh = (double)s * sqrt((double)cc);
+      const double eq = xm * sqrt(ey) + em * yh;
+      const float e2 = f32_up((2.0 * eq + 4e-7 * (xm + em) * yh) * (1.0 + 1e-5) / (double)sd);
+      e2_lds[qi] = s > 0.f ? e2 : 0.f;
+    }
+  };
+  if (!(force & 4)) {
+    if (w < NQT) quant(w, y0, am0);
+    for (int qi = w + 4; qi < NQT; qi += 4) {  // nq 5..8 only
+      const int qq = qi < nq ? qi : nq - 1;
+      const float qm = qi < nq ? 1.f : 0.f;
       float y[PL];
       float am = 0.f;
 #pragma unroll
       for (int e = 0; e < PL; ++e) {
-        y[e] = qi == w ? y0[e] : qi < nq ? qelem<DT>(Q, (int64_t)qi * D + lane + 64 * e) : 0.f;
+        y[e] = qelem<DT>(Q, (int64_t)qq * D + lane + 64 * e) * qm;
         am = fmaxf(am, fabsf(y[e]));
       }
-#pragma unroll
-      for (int off = 32; off; off >>= 1) am = fmaxf(am, __shfl_xor(am, off));
-      const float s = am > 0.f ? __fdiv_rn(am, 127.f) : 0.f;
-      double ey = 0.0;
-      long long cc = 0;
-#pragma unroll
-      for (int e = 0; e < PL; ++e) {
-        int c = 0;
-        if (s > 0.f) c = (int)fminf(fmaxf(rintf(__fdiv_rn(y[e], s)), -127.f), 127.f);
-        qc_lds[qi][lane + 64 * e] = (int8_t)c;
-        const double dd = (double)y[e] - (double)s * (double)c;
-        ey += dd * dd;
-        cc += (long long)c * c;
-      }
-#pragma unroll
-      for (int off = 32; off; off >>= 1) {
-        ey += __shfl_xor(ey, off);
-        cc += __shfl_xor(cc, off);
-      }
-      if (lane == 0) {
-        float e2 = 0.f;
-        if (s > 0.f) {
-          const double yh = (double)s * sqrt((double)cc);
-          const double eq = xm * sqrt(ey) + em * yh;
-          e2 = f32_up((2.0 * eq + 4e-7 * (xm + em) * yh) * (1.0 + 1e-5) / (double)s);
-        }
-        e2_lds[qi] = e2;
-      }
+      am = wave_max_f32(am);
+      quant(qi, y, am);
     }
   }
   __syncthreads();
@@ -277,8 +291,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       mk[qi][w * kK + lane] = v ? ((uint64_t)ord_f32(L[qi].ls) << 32) | (uint32_t)(~(uint32_t)L[qi].lr) : 0ull;
     }
     float d = dm[qi];
-#pragma unroll
-    for (int off = 32; off; off >>= 1) d = fmaxf(d, __shfl_xor(d, off));
+    d = wave_max_f32(d);
     if (lane == 0) wdm[w][qi] = d;
   }
   __syncthreads();
@@ -293,8 +306,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     // the drop bound instead)
     float d = fmaxf(fmaxf(wdm[0][qi], wdm[1][qi]), fmaxf(wdm[2][qi], wdm[3][qi]));
     if (v && rank >= kK - 1) d = fmaxf(d, ms_);
-#pragma unroll
-    for (int off = 32; off; off >>= 1) d = fmaxf(d, __shfl_xor(d, off));
+    d = wave_max_f32(d);
     const int nv = (int)__popcll(__ballot(v));
     const int64_t o0 = ((int64_t)qi * n_lists + blockIdx.x) * kK;
     if (v && rank < kK - 1) {
@@ -341,8 +353,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   __shared__ float red[4];
   __shared__ int n_sv, fail;
   __shared__ float cut;
-  __shared__ uint32_t lbk_o;
-  __shared__ __attribute__((aligned(16))) uint32_t hk[1024];
+  __shared__ uint32_t fin[4 * kK];
   if (tid == 0) fail = force & 1;
   for (int qi = 0; qi < nq; ++qi) {
     // bulk copy into LDS with 8 loads per thread in flight (agent-scope loads are not batched by the
@@ -371,65 +382,87 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     if (tid == 0) n_sv = 0;
     __syncthreads();
     if (qi == 0) RFX_K11_L(1);
-    // The largest drop bound, and LB, a lower bound of a_k from each record's best entry (every entry
-    // when the records are few): distinct live rows either way.
+    // The largest drop bound (entry 15 of each record), and LB, a lower bound of a_k: the k-th largest
+    // key (with multiplicity; 0 = fewer than k) of the records' best entries (every entry when the
+    // records are few) — distinct live rows either way.  Each wave extracts the k best of its 256 keys
+    // (4 per lane, sorted in registers) by k rounds of a wave max; wave 0 ranks the 4k finalists (the
+    // union of the waves' top-k holds the top-k values with their multiplicity).
     float dmax = -__builtin_inff();
-    for (int i = tid; i < n; i += 256)
+    for (int c = tid; c < n_lists; c += 256) {
+      const int i = c * kK + kK - 1;
       if (br[i] == kDropRow) dmax = fmaxf(dmax, bs[i]);
-#pragma unroll
-    for (int off = 32; off; off >>= 1) dmax = fmaxf(dmax, __shfl_xor(dmax, off));
+    }
+    dmax = wave_max_f32(dmax);
     if (lane == 0) red[w] = dmax;
-    // heads (or every entry when the records are few) as orderable keys, 0 = none; LB = the best key
-    // with at least k keys at or above it (k distinct live rows reach it): every thread counts for
-    // its key with 16-B broadcast reads of the whole key array, no dependent loads
     const bool every = n <= 1024;
     const int m = (force & 32) ? 0 : every ? n : n_lists;  // <= 1024
-    for (int c = tid; c < 1024; c += 256) {
-      uint32_t key = 0u;
-      if (c < m) {
-        const int i = every ? c : c * kK;
-        const int r = br[i];
-        key = r != kEmptyRow && r != kDropRow ? ord_f32(bs[i]) : 0u;
-      }
-      hk[c] = key;
-    }
-    if (tid == 0) lbk_o = 0u;
-    __syncthreads();
     {
-      uint32_t cand = 0u;
-      const uint4* hk4 = (const uint4*)hk;
+      uint32_t a0, a1, a2, a3;
+      uint32_t ak[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const uint32_t mine = hk[tid + 256 * u];
-        if (mine) {
-          int cnt = 0;
-#pragma unroll 8
-          for (int i = 0; i < (m + 3) / 4; ++i) {
-            const uint4 v = hk4[i];
-            cnt += (v.x >= mine) + (v.y >= mine) + (v.z >= mine) + (v.w >= mine);
-          }
-          if (cnt >= k_out) cand = max(cand, mine);
+        const int c = w * 256 + u * 64 + lane;
+        uint32_t key = 0u;
+        if (c < m) {
+          const int i = every ? c : c * kK;
+          const int r = br[i];
+          key = r != kEmptyRow && r != kDropRow ? ord_f32(bs[i]) : 0u;
         }
+        ak[u] = key;
       }
-#pragma unroll
-      for (int off = 32; off; off >>= 1) cand = max(cand, (uint32_t)__shfl_xor((int)cand, off));
-      if (lane == 0 && cand) atomicMax(&lbk_o, cand);
+      // sort the lane's four keys descending (five compare-exchanges)
+      auto cx = [](uint32_t& x, uint32_t& y) {
+        const uint32_t hi = max(x, y), lo = min(x, y);
+        x = hi;
+        y = lo;
+      };
+      cx(ak[0], ak[1]);
+      cx(ak[2], ak[3]);
+      cx(ak[0], ak[2]);
+      cx(ak[1], ak[3]);
+      cx(ak[1], ak[2]);
+      a0 = ak[0], a1 = ak[1], a2 = ak[2], a3 = ak[3];
+      if (lane < kK) fin[w * kK + lane] = 0u;
+      for (int it = 0; it < k_out; ++it) {
+        const uint32_t mx = wave_max_u32(a0);
+        const bool win = lane == (int)__builtin_ctzll(__ballot(a0 == mx));
+        a0 = win ? a1 : a0;
+        a1 = win ? a2 : a1;
+        a2 = win ? a3 : a2;
+        a3 = win ? 0u : a3;
+        if (lane == 0) fin[w * kK + it] = mx;
+      }
     }
     __syncthreads();
-    if (tid == 0) {
-      const float dm_all = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-      cut = lbk_o ? unord_f32(lbk_o) - e2_lds[qi] : -__builtin_inff();
-      // a dropped row at or above LB - e2 could belong to the top-k: not proven
-      if (dm_all > -__builtin_inff() && dm_all >= cut) fail = 1;
+    if (w == 0) {
+      const uint32_t x = fin[lane];  // 4 kK = 64 finalists, one per lane
+      int ge = 0, gt = 0;
+#pragma unroll 16
+      for (int i = 0; i < 4 * kK; ++i) {
+        const uint32_t v = fin[i];
+        ge += v >= x ? 1 : 0;
+        gt += v > x ? 1 : 0;
+      }
+      uint32_t lb = x && gt < k_out && ge >= k_out ? x : 0u;
+      lb = wave_max_u32(lb);
+      if (lane == 0) {
+        const float dm_all = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+        cut = lb ? unord_f32(lb) - e2_lds[qi] : -__builtin_inff();
+        // a dropped row at or above LB - e2 could belong to the top-k: not proven
+        if (dm_all > -__builtin_inff() && dm_all >= cut) fail = 1;
+      }
     }
     __syncthreads();
     if (qi == 0) RFX_K11_L(2);
-#pragma unroll 4
-    for (int i = tid; i < n; i += 256) {
-      const int r = br[i];
-      if (r != kEmptyRow && r != kDropRow && bs[i] >= cut) {
+    // survivors: the entries at or above the cut; a record is sorted best first, so its scan ends at
+    // the first entry below the cut (most records: at their best entry)
+    for (int c = tid; c < n_lists; c += 256) {
+      const int i0 = c * kK;
+      for (int e = 0; e < kK - 1; ++e) {
+        const int r = br[i0 + e];
+        if (r == kEmptyRow || !(bs[i0 + e] >= cut)) break;
         const int j2 = atomicAdd(&n_sv, 1);
-        if (j2 < kSurvCap) sv[j2] = i;
+        if (j2 < kSurvCap) sv[j2] = i0 + e;
       }
     }
     __syncthreads();
@@ -468,8 +501,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
           for (int u = 0; u < VPL; ++u)
 #pragma unroll
             for (int ee = 0; ee < EPV; ++ee) acc += (double)elem<DT>(xv[ur][u], ee) * (double)elem<DT>(yv[u], ee);
-#pragma unroll
-          for (int off = 8; off; off >>= 1) acc += __shfl_xor(acc, off);  // within the 16-lane group
+          acc = row16_sum_f64(acc);  // within the 16-lane group (DPP; lane 0's sum = the xor butterfly's)
           if (gl == 0 && e < ns)
             skey[e] = ((uint64_t)ord_f32((float)acc) << 32) | (uint32_t)(~(uint32_t)br[sv[e]]);
         }

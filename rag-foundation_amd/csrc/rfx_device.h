@@ -97,6 +97,62 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// Wave reductions without ds_bpermute: a __shfl_xor is an LDS-crossbar round trip (~100 cycles with
+// its wait), six of them per reduction.  DPP row_ror within each 16-lane row (every lane receives
+// its row's result), then the four row results by readlane; every lane receives the wave's result.
+// For lane 0 of a row, row_ror in the order 8, 4, 2, 1 pairs the same partial sums as a xor
+// butterfly in that order, so row16_sum_f64's lane-0 sum equals the __shfl_xor version bit for bit.
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x122, 0xf, 0xf, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x121, 0xf, 0xf, false));
+  const uint32_t a = __builtin_amdgcn_readlane((int)v, 0), b = __builtin_amdgcn_readlane((int)v, 16);
+  const uint32_t c = __builtin_amdgcn_readlane((int)v, 32), d = __builtin_amdgcn_readlane((int)v, 48);
+  return max(max(a, b), max(c, d));
+}
+__device__ __forceinline__ float wave_max_f32(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xf, 0xf, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xf, 0xf, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x122, 0xf, 0xf, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x121, 0xf, 0xf, false)));
+  return fmaxf(fmaxf(readlane_f(v, 0), readlane_f(v, 16)), fmaxf(readlane_f(v, 32), readlane_f(v, 48)));
+}
+__device__ __forceinline__ double row16_sum_f64(double v) {
+#define RFX_DPP_F64_STEP(ctl)                                                                       \
+  {                                                                                                 \
+    const long long b = __double_as_longlong(v);                                                    \
+    const int lo = __builtin_amdgcn_mov_dpp((int)b, ctl, 0xf, 0xf, false);                          \
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), ctl, 0xf, 0xf, false);                  \
+    v += __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));          \
+  }
+  RFX_DPP_F64_STEP(0x128)
+  RFX_DPP_F64_STEP(0x124)
+  RFX_DPP_F64_STEP(0x122)
+  RFX_DPP_F64_STEP(0x121)
+#undef RFX_DPP_F64_STEP
+  return v;
+}
+__device__ __forceinline__ double wave_sum_f64(double v) {
+  v = row16_sum_f64(v);
+  const long long b = __double_as_longlong(v);
+  double s = 0.0;
+#pragma unroll
+  for (int r = 0; r < 64; r += 16) {
+    const uint32_t lo = __builtin_amdgcn_readlane((int)b, r), hi = __builtin_amdgcn_readlane((int)(b >> 32), r);
+    s += __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+  }
+  return s;
+}
+__device__ __forceinline__ int wave_sum_i32(int v) {
+  v += __builtin_amdgcn_mov_dpp(v, 0x128, 0xf, 0xf, false);
+  v += __builtin_amdgcn_mov_dpp(v, 0x124, 0xf, 0xf, false);
+  v += __builtin_amdgcn_mov_dpp(v, 0x122, 0xf, 0xf, false);
+  v += __builtin_amdgcn_mov_dpp(v, 0x121, 0xf, 0xf, false);
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+         __builtin_amdgcn_readlane(v, 48);
+}
+
 // lane l receives lane l-1's value (lane 0 keeps its own): one DPP move (wave_shr:1, GFX9 DPP)
 // instead of a ds_bpermute round trip through the LDS crossbar — the list insert's critical path.
 __device__ __forceinline__ int lane_shr1(int v) { return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xf, 0xf, false); }
