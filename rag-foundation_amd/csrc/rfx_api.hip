@@ -1185,10 +1185,26 @@ int rfx_dbg_screen_variant(rfx_index_t h, const void* queries_d, int64_t nq, int
   uint32_t* stau = (uint32_t*)(ws + L.s_tau);
   rfx::launch_screen_queries(queries_d, ix->dtype, ix->dim, nq, L.sp.nq_pad, qc, qe2, ix->sstats, stau,
                              (uint32_t*)(ws + L.s_gate), nullptr, st);
+  // RFX_DBG_KEEP_TAU=1: the slot table starts from the previous launch's final one (the same queries on
+  // the same rows: still a lower bound of a_k) — the timing of a bound with no warm-up at all
+  static const bool keep_tau = getenv("RFX_DBG_KEEP_TAU") != nullptr;
+  static uint32_t* tau_saved = nullptr;
+  static size_t tau_saved_bytes = 0;
+  const size_t tb = rfx::tau_bytes_screen(L.sp);
+  if (keep_tau) {
+    if (tau_saved_bytes < tb) {
+      if (tau_saved) RFX_HIP(hipFree(tau_saved));
+      RFX_HIP(hipMalloc(&tau_saved, tb));
+      RFX_HIP(hipMemsetAsync(tau_saved, 0, tb, st));
+      tau_saved_bytes = tb;
+    }
+    RFX_HIP(hipMemcpyAsync(stau, tau_saved, tb, hipMemcpyDeviceToDevice, st));
+  }
   if (rfx::launch_scan_screen_dbg(L.sp, variant, ix->scodes, ix->smeta, ix->sstats, (int)ix->rows, qc, qe2, (int)nq, stau,
                                   (float*)(ws + L.s_cs), (int*)(ws + L.s_cr), (uint32_t*)(ws + L.s_drop), st) != 0)
     return fail(RFX_EUNSUPPORTED, "screen variant %d unsupported", variant);
   RFX_HIP(hipGetLastError());
+  if (keep_tau) RFX_HIP(hipMemcpyAsync(tau_saved, stau, tb, hipMemcpyDeviceToDevice, st));
   return RFX_OK;
 }
 
