@@ -2,8 +2,10 @@
 // two-pass scan's int8 screen (k_scan_screen.h MODE bits: 1 no top-k fold, 2 no launder, 4 prefetch
 // distance 1, 8 no corpus stream, 16 early slot-table refreshes, 32 slow-path entry count, 64 store-wide
 // integer fast-path bound, 128 epilogue in place, 256 min-of-KL slot bound, 512 slow path never taken,
-// 1024 serial LDS insert, 2048 slow-path issue priority, 32768 no stage barriers),
+// 1024 serial LDS insert, 2048 slow-path issue priority, 32768 no stage barriers, 65536 per-block
+// start / end wall clocks),
 // via rfx_dbg_screen_variant; variant = 100000 * RING + MODE (RING in {4, 6, 8, 10, 12}).
+#define RFX_K10_BLOCK_TIMES
 #include "k_scan_screen.h"
 
 namespace rfx {
@@ -51,11 +53,16 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
     RFX_K10V(10, 32768)
     RFX_K10V(10, 32800)
     RFX_K10V(12, 32768)
+    RFX_K10V(8, 65536)
     default:
       return -1;
   }
 #undef RFX_K10V
   return 0;
+}
+
+int dbg_k10_block_times(unsigned long long* out_h) {
+  return hipMemcpyFromSymbol(out_h, HIP_SYMBOL(k10::g_k10_bt), sizeof(k10::g_k10_bt)) == hipSuccess ? 0 : -1;
 }
 
 }  // namespace rfx

@@ -57,6 +57,11 @@ constexpr int kTauW = 16;                 // u32 per query in the threshold tabl
 constexpr int kTauBytes = kQG * kTauW * 4;  // 16 KB
 constexpr int kTauGPW = kTauBytes / 1024 / kWaves;
 constexpr int kMR = 8;  // tile-metadata slots (1 KB each: 64 lane copies of the 16-B record)
+#ifdef RFX_K10_BLOCK_TIMES
+// debug build only (k10_dbg.hip): MODE 65536 records each block's 100-MHz wall clock when it starts
+// and when all its waves are done (tools/k10_variants.py --block-times)
+__device__ unsigned long long g_k10_bt[1024][2];
+#endif
 template <int RING>
 constexpr int meta_off() { return RING * kSlot; }
 template <int RING>
@@ -294,6 +299,10 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   const int nt = range < ntiles ? (ntiles - range + nblk - 1) / nblk : 0;
   const int S = nt * NST;
   if (S == 0) return;
+#ifdef RFX_K10_BLOCK_TIMES
+  if constexpr ((MODE & 65536) != 0)
+    if (tid == 0 && range < 1024 && blockIdx.y == 0) g_k10_bt[range][0] = wall_clock64();
+#endif
   const int lst = range * 2 + half;
   const float e2 = qe2[q];
   const float smax = __uint_as_float(stats[2]);  // max tile scale of the store
@@ -624,6 +633,13 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
     }
     drops[(int64_t)q * n_lists + lst] = drop;
   }
+#ifdef RFX_K10_BLOCK_TIMES
+  if constexpr ((MODE & 65536) != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0 && range < 1024 && blockIdx.y == 0) g_k10_bt[range][1] = wall_clock64();
+  }
+#endif
 }
 
 // one translation unit per D instantiates the kernel for KL in {4, 10}, with and without a filter mask

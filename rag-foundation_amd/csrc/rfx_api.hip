@@ -1156,6 +1156,7 @@ int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k
 namespace rfx {
 int dbg_select_times(unsigned long long* out_h);
 int dbg_k11_times(unsigned long long* blocks_h, unsigned long long* last_h);
+int dbg_k10_block_times(unsigned long long* out_h);
 constexpr int k10_tau_words() { return 16; }  // k_scan_screen.h kTauW
 int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, const void* tmv, const uint32_t* sts,
                            int nrows, const int8_t* Qc, const float* qe2, int nq, uint32_t* tau, float* cs, int* cr,
@@ -1267,6 +1268,14 @@ int rfx_dbg_screen_counts(rfx_index_t h, int64_t nq, int k, const void* ws_d, ui
 int rfx_dbg_select_times(unsigned long long* out_h) {
   if (!out_h) return fail(RFX_EINVAL, "null out");
   if (rfx::dbg_select_times(out_h) != 0) return fail(RFX_EDEVICE, "hipMemcpyFromSymbol failed");
+  return RFX_OK;
+}
+
+// Diagnostic: kernel 10's per-block wall clocks of the last MODE-65536 variant launch (k10_dbg.hip
+// g_k10_bt: [1024][2] u64 start / end, 100 MHz).
+int rfx_dbg_k10_block_times(unsigned long long* out_h) {
+  if (!out_h) return fail(RFX_EINVAL, "null out");
+  if (rfx::dbg_k10_block_times(out_h) != 0) return fail(RFX_EDEVICE, "hipMemcpyFromSymbol failed");
   return RFX_OK;
 }
 
