@@ -2,8 +2,8 @@
 // two-pass scan's int8 screen (k_scan_screen.h MODE bits: 1 no top-k fold, 2 no launder, 4 prefetch
 // distance 1, 8 no corpus stream, 16 early slot-table refreshes, 32 slow-path entry count, 64 store-wide
 // integer fast-path bound, 128 epilogue in place, 256 min-of-KL slot bound, 512 slow path never taken,
-// 1024 serial LDS insert, 2048 slow-path issue priority, 32768 no stage barriers, 65536 per-block
-// start / end wall clocks),
+// 1024 serial LDS insert, 2048 slow-path issue priority, 4096 static tile split (no XCD balance),
+// 32768 no stage barriers, 65536 per-block start / end wall clocks),
 // via rfx_dbg_screen_variant; variant = 100000 * RING + MODE (RING in {4, 6, 8, 10, 12}).
 #define RFX_K10_BLOCK_TIMES
 #include "k_scan_screen.h"
@@ -20,7 +20,8 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
 #define RFX_K10V(R, M)                                                                                        \
   case 100000 * R + M:                                                                                          \
     hipLaunchKernelGGL((k10::scan_screen_kernel<10, 768, false, R, M>), grid, dim3(512), 0, st, X, tm, sts, Qc, \
-                       qe2, nq, ntiles, tau, cs, cr, dr, p.n_lists, nullptr);                                \
+                       qe2, nq, ntiles, tau, cs, cr, dr, p.n_lists, nullptr, tau + p.nq_pad * k10::kTauW,      \
+                       xcd_weights_device_ptr());                                                             \
     break;
   switch (variant) {
     RFX_K10V(4, 0)
@@ -54,6 +55,8 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
     RFX_K10V(10, 32800)
     RFX_K10V(12, 32768)
     RFX_K10V(8, 65536)
+    RFX_K10V(8, 4096)
+    RFX_K10V(8, 4096 + 65536)
     default:
       return -1;
   }

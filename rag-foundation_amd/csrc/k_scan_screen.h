@@ -57,6 +57,7 @@ constexpr int kTauW = 16;                 // u32 per query in the threshold tabl
 constexpr int kTauBytes = kQG * kTauW * 4;  // 16 KB
 constexpr int kTauGPW = kTauBytes / 1024 / kWaves;
 constexpr int kMR = 8;  // tile-metadata slots (1 KB each: 64 lane copies of the 16-B record)
+constexpr int kXbWords = 8;  // after the slot table: the XCD split's weight snapshot for this launch
 #ifdef RFX_K10_BLOCK_TIMES
 // debug build only (k10_dbg.hip): MODE 65536 records each block's 100-MHz wall clock when it starts
 // and when all its waves are done (tools/k10_variants.py --block-times)
@@ -278,7 +279,8 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
                                                              int nq, int ntiles, uint32_t* __restrict__ tau,
                                                              float* __restrict__ cand_s, int* __restrict__ cand_r,
                                                              uint32_t* __restrict__ drops, int64_t n_lists,
-                                                             const uint32_t* __restrict__ mask) {
+                                                             const uint32_t* __restrict__ mask, uint32_t* __restrict__ xb,
+                                                             uint32_t* __restrict__ xw) {
   constexpr int NKS = D / 64;    // 64-deep k-steps per tile
   constexpr int NST = D / kSK;   // stages per tile
   constexpr int KPS = kSK / 64;  // k-steps per stage (4)
@@ -296,8 +298,36 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   const int qg = blockIdx.y * kQG;
   const int q = qg + w * kQW + 16 * ((lane >> 4) & 1) + (lane & 15);  // after the pair swap
   const int nblk = gridDim.x;
-  const int nt = range < ntiles ? (ntiles - range + nblk - 1) / nblk : 0;
+  // The tiles of this block: tb0 + i * tstride, i < nt.  Static split: tiles range, range + nblk, ...
+  // XCD-balanced split (production; debug MODE 4096 keeps the static one): block b runs on XCD b % 8, and
+  // the XCDs do not run at one speed under the power limit (2.10 to 2.20 ms per block at
+  // 10M rows, the slow XCD's blocks last in every launch).  XCD x takes the tile range
+  // [T_x, T_x+1) in proportion to its weight (the speed it measured in earlier launches, a snapshot
+  // the query quantiser took for this launch, so every block computes the same split), its 32 blocks
+  // interleaved in it.  Any split of the tiles into disjoint lists is exact.
+  // (>= 64 tiles per block on average: with weights in [0.5, 2] every block keeps >= 2 tiles)
+  const bool bal = (MODE & 4096) == 0 && xb != nullptr && xw != nullptr && (nblk & 7) == 0 && ntiles >= 64 * nblk;
+  const int xc = range & 7;
+  int tb0 = range, tstride = nblk, nt = range < ntiles ? (ntiles - range + nblk - 1) / nblk : 0;
+  if (bal) {
+    uint64_t pre = 0, tot = 0;
+    uint32_t wx = 1;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+      const uint32_t wv = xb[x];  // (1024 = 1.0, clamped by the quantiser to [512, 2048])
+      pre += x < xc ? wv : 0u;
+      wx = x == xc ? wv : wx;
+      tot += wv;
+    }
+    const int t_lo = (int)((uint64_t)ntiles * pre / tot), t_hi = (int)((uint64_t)ntiles * (pre + wx) / tot);
+    const int bpx = nblk >> 3;
+    tb0 = t_lo + (range >> 3);
+    tstride = bpx;
+    nt = tb0 < t_hi ? (t_hi - tb0 + bpx - 1) / bpx : 0;
+  }
+  auto tile_of = [&](int i) -> int { return tb0 + i * tstride; };
   const int S = nt * NST;
+  const uint64_t t_start = wall_clock64();
   if (S == 0) return;
 #ifdef RFX_K10_BLOCK_TIMES
   if constexpr ((MODE & 65536) != 0)
@@ -339,7 +369,6 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   const int pr = 4 * w + (lane >> 4);
   const uint32_t laneoff = (uint32_t)(pr * D + (((lane & 15) ^ (pr & 15)) * 16));
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
-  const int64_t tile_stride = (int64_t)nblk * kTM * D;
   // The tile metadata (scale, live word) rides the same counted stream: with the piece of a tile's
   // first stage, every wave also DMAs the tile's 16-B record (64 lane copies, identical bytes from
   // every wave) into meta slot (tile % kMR), read by the epilogue's slow path from LDS.
@@ -349,12 +378,12 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
     gi = gi < S ? gi : S - 1;  // tail: harmless duplicate loads keep the counted waits exact
     const int ti = gi / NST;
     const int si = gi - ti * NST;
-    const int8_t* tbase = X + (int64_t)range * kTM * D + ti * tile_stride + si * kSK;
+    const int8_t* tbase = X + (int64_t)tile_of(ti) * kTM * D + si * kSK;
     const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)(slot * kSlot) + (uint32_t)(w * 1024));
     bdma_nt(make_rsrc(tbase), laneoff, dst);  // codes are read once per batch
     if (first) {
       const uint32_t mdst = __builtin_amdgcn_readfirstlane(lds_base + kMetaOff + (uint32_t)((ti % kMR) * 1024));
-      bdma(meta_rsrc, (uint32_t)(range + ti * nblk) * 16u, mdst);
+      bdma(meta_rsrc, (uint32_t)tile_of(ti) * 16u, mdst);
     }
   };
   const v4i32 tau_rsrc = make_rsrc(tau);
@@ -455,7 +484,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   // waiting for the MFMA pipeline to drain at every tile end (debug MODE 128: epilogue in place).
   v4i32 accA[4], accB[4];  // [rb * 2 + qb]
   auto epilogue = [&](const int it, v4i32(&acc4)[4]) {
-    const int tile = range + it * nblk;
+    const int tile = tile_of(it);
     // Fast path: the max D of each of the lane's two queries, scaled by the tile's scale, against the
     // query's bound (qb 0 values in acc4[0], acc4[2]; qb 1 in acc4[1], acc4[3]).  Only when some lane of the wave
     // may hold a row to look at: the tile's scale and live word (LDS metadata slot), the pair swap (even
@@ -633,6 +662,15 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
     }
     drops[(int64_t)q * n_lists + lst] = drop;
   }
+  if (bal && blockIdx.y == 0 && tid == 0) {
+    // speed bookkeeping for the next launches' split: the block's duration (wave 0's view) and tiles,
+    // added to its XCD's sums (fire-and-forget atomics: no wait, nothing orders on them); the next
+    // query quantiser turns the sums into weights (k_screen.hip)
+    const uint64_t dt = wall_clock64() - t_start;
+    __hip_atomic_fetch_add(xw + 8 + xc, (uint32_t)(dt < 0xffffffull ? dt : 0xffffffull), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(xw + 16 + xc, (uint32_t)nt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 #ifdef RFX_K10_BLOCK_TIMES
   if constexpr ((MODE & 65536) != 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -646,19 +684,19 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
 #define RFX_K10_INSTANTIATE(DV, NAME)                                                                         \
   int NAME(int kl, dim3 grid, hipStream_t st, const int8_t* X, const uint4* tm, const uint32_t* sts,           \
            const int8_t* Qc, const float* qe2, int nq, int ntiles, uint32_t* tau, float* cs, int* cr,          \
-           uint32_t* dr, int64_t n_lists, const uint32_t* mask) {                                            \
+           uint32_t* dr, int64_t n_lists, const uint32_t* mask, uint32_t* xb, uint32_t* xw) {               \
     if (kl == 4 && !mask)                                                                                   \
       hipLaunchKernelGGL((scan_screen_kernel<4, DV, false>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,   \
-                         ntiles, tau, cs, cr, dr, n_lists, mask);                                            \
+                         ntiles, tau, cs, cr, dr, n_lists, mask, xb, xw);                                    \
     else if (kl == 10 && !mask)                                                                             \
       hipLaunchKernelGGL((scan_screen_kernel<10, DV, false>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,  \
-                         ntiles, tau, cs, cr, dr, n_lists, mask);                                            \
+                         ntiles, tau, cs, cr, dr, n_lists, mask, xb, xw);                                    \
     else if (kl == 4)                                                                                       \
       hipLaunchKernelGGL((scan_screen_kernel<4, DV, true>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,    \
-                         ntiles, tau, cs, cr, dr, n_lists, mask);                                            \
+                         ntiles, tau, cs, cr, dr, n_lists, mask, xb, xw);                                    \
     else if (kl == 10)                                                                                      \
       hipLaunchKernelGGL((scan_screen_kernel<10, DV, true>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,   \
-                         ntiles, tau, cs, cr, dr, n_lists, mask);                                            \
+                         ntiles, tau, cs, cr, dr, n_lists, mask, xb, xw);                                    \
     else                                                                                                    \
       return -1;                                                                                            \
     return 0;                                                                                               \

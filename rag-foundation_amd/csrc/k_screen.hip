@@ -13,7 +13,7 @@ namespace k10 {
 #define RFX_K10_DECL(NAME)                                                                                    \
   int NAME(int kl, dim3 grid, hipStream_t st, const int8_t* X, const uint4* tm, const uint32_t* sts,           \
            const int8_t* Qc, const float* qe2, int nq, int ntiles, uint32_t* tau, float* cs, int* cr,          \
-           uint32_t* dr, int64_t n_lists, const uint32_t* mask);
+           uint32_t* dr, int64_t n_lists, const uint32_t* mask, uint32_t* xb, uint32_t* xw);
 RFX_K10_DECL(launch_768)
 RFX_K10_DECL(launch_1024)
 #undef RFX_K10_DECL
@@ -155,16 +155,52 @@ __global__ __launch_bounds__(256) void screen_quantize_kernel(const void* __rest
 // 4e-7 term covers the f32 roundings of A = s_t D (2^-24 relative, twice) and of the bound
 // subtraction, the 1e-5 the f64 norms.  Also zeroes the query's threshold slots and (block 0) the
 // fallback gate.  Padded queries (q >= nq) get code 0 and e2 0.
+// Kernel 10's XCD table, one per device (k_scan_screen.h: the tile split across the 8 XCDs): [0, 8)
+// weights (1024 = 1.0, 0 = not measured yet), [8, 16) the blocks' durations (10-ns ticks) and [16, 24)
+// their tiles per XCD, summed by kernel 10 since the last query quantiser.
+__device__ uint32_t g_xcd_w[24];
+
 template <int DT, int D>
 __global__ __launch_bounds__(256) void screen_queries_kernel(const uint16_t* __restrict__ Q, int nq, int nq_pad,
                                                              int8_t* __restrict__ Qc, float* __restrict__ qe2,
                                                              const uint32_t* __restrict__ stats,
                                                              uint32_t* __restrict__ tau, uint32_t* __restrict__ gate,
-                                                             uint32_t* __restrict__ ftau) {
+                                                             uint32_t* __restrict__ ftau, uint32_t* __restrict__ xb) {
   constexpr int NM = D / 256;
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x == 0) *gate = 0u;
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    // Kernel 10's split for this launch (lanes 0..7 = XCDs): the speed each XCD measured since the last
+    // quantiser (tiles per tick, the sums taken and reset), its weight moved half-way to its share of
+    // the mean speed (clamped to [0.5, 2]); the snapshot in the workspace is what every block of this
+    // launch reads.  Concurrent launches on other streams only blur the measurement.
+    const int x = threadIdx.x;
+    uint32_t d = 0u, n = 0u, w = 1024u;
+    if (x < 8) {
+      d = __hip_atomic_exchange(&g_xcd_w[8 + x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      n = __hip_atomic_exchange(&g_xcd_w[16 + x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      w = __hip_atomic_load(&g_xcd_w[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      w = w == 0u ? 1024u : w < 512u ? 512u : w > 2048u ? 2048u : w;
+    }
+    const float sp = d && n ? (float)n / (float)d : 0.f;
+    float sum = sp;
+    int have = x < 8 && sp > 0.f ? 1 : 0;
+#pragma unroll
+    for (int off = 1; off < 8; off <<= 1) {
+      sum += __shfl_xor(sum, off);
+      have += __shfl_xor(have, off);
+    }
+    if (x < 8) {
+      if (have == 8 && sum > 0.f) {
+        const float want = fminf(fmaxf(1024.f * sp / (0.125f * sum), 512.f), 2048.f);
+        w = (uint32_t)(0.5f * ((float)w + want));
+        w = w < 512u ? 512u : w > 2048u ? 2048u : w;
+        __hip_atomic_store(&g_xcd_w[x], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      xb[x] = w;
+    }
+  }
   if (q >= nq_pad) return;
   if (lane < k10::kTauW) tau[(int64_t)q * k10::kTauW + lane] = 0u;
   if (ftau && lane < kFallbackTauW) ftau[(int64_t)q * kFallbackTauW + lane] = 0u;  // the gated fallback's table
@@ -457,14 +493,25 @@ MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k, in
   return p;
 }
 
-size_t tau_bytes_screen(const MfmaPlan& p) { return (size_t)p.nq_pad * k10::kTauW * sizeof(uint32_t); }
+// the slot table [nq_pad][16], then kernel 10's XCD-split words (k10::kXbWords)
+size_t tau_bytes_screen(const MfmaPlan& p) {
+  return ((size_t)p.nq_pad * k10::kTauW + k10::kXbWords) * sizeof(uint32_t);
+}
+
+uint32_t* xcd_weights_device_ptr() {
+  static uint32_t* ptr[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!ptr[dev] && hipGetSymbolAddress((void**)&ptr[dev], HIP_SYMBOL(g_xcd_w)) != hipSuccess) ptr[dev] = nullptr;
+  return ptr[dev];
+}
 
 void launch_screen_queries(const void* Q, int dtype, int D, int64_t nq, int64_t nq_pad, int8_t* Qc, float* qe2,
                            const uint32_t* stats, uint32_t* tau, uint32_t* gate, uint32_t* ftau, hipStream_t st) {
   const dim3 grid((unsigned)((nq_pad + 3) / 4));
 #define RFX_SQQ(DTV, DV)                                                                                       \
   hipLaunchKernelGGL((screen_queries_kernel<DTV, DV>), grid, dim3(256), 0, st, (const uint16_t*)Q, (int)nq,      \
-                     (int)nq_pad, Qc, qe2, stats, tau, gate, ftau)
+                     (int)nq_pad, Qc, qe2, stats, tau, gate, ftau, tau + nq_pad * k10::kTauW)
   if (dtype == RFX_BF16 && D == 768)
     RFX_SQQ(RFX_BF16, 768);
   else if (dtype == RFX_BF16)
@@ -484,7 +531,7 @@ int launch_scan_screen(const MfmaPlan& p, const int8_t* codes, const void* tmeta
   dim3 grid(p.blocks, p.q_blocks);
   auto f = D == 768 ? k10::launch_768 : k10::launch_1024;
   return f(p.k_lane, grid, st, codes, (const uint4*)tmeta, stats, Qc, qe2, nq, ntiles, tau, cs, cr, drops, p.n_lists,
-           mask);
+           mask, tau + p.nq_pad * k10::kTauW, xcd_weights_device_ptr());
 }
 
 int launch_screen_select(const float* cs, const int* cr, const uint32_t* drops, int64_t n_lists, int list_len,

@@ -145,6 +145,7 @@ void launch_screen_quantize(const void* X, int D, int dtype, int64_t tile0, int6
                             int8_t* codes, void* tmeta, uint32_t* stats, hipStream_t st);
 MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k, int max_blocks = 0);
 size_t tau_bytes_screen(const MfmaPlan& p);
+uint32_t* xcd_weights_device_ptr();  // kernel 10's per-device XCD weight table (k_screen.hip g_xcd_w)
 // ftau (or null): the gated fallback scan's threshold table ([nq_pad][kFallbackTauW], kernel 6 / 8),
 // zeroed here so the fallback launch needs no memset of its own (tau_zeroed below)
 constexpr int kFallbackTauW = 16;

@@ -24,6 +24,7 @@ ap.add_argument("--rows", type=int, default=1_250_000)
 ap.add_argument("--nq", type=int, default=256)
 ap.add_argument("--k", type=int, default=10)
 ap.add_argument("--reps", type=int, default=20)
+ap.add_argument("--variant", type=int, default=865536, help="865536 = production split + clocks; 869632 = static split")
 a = ap.parse_args()
 f = _lib.lib.rfx_dbg_screen_variant
 f.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -41,7 +42,7 @@ st = _lib.stream_ptr()
 ntiles = -(-a.rows // 32)
 recs = []
 for rep in range(a.reps):
-    _lib.check(f(ix.handle, _lib.ptr(q), a.nq, a.k, 865536, _lib.ptr(ws), ws.numel(), st))
+    _lib.check(f(ix.handle, _lib.ptr(q), a.nq, a.k, a.variant, _lib.ptr(ws), ws.numel(), st))
     torch.cuda.synchronize()
     bt = np.zeros((1024, 2), dtype=np.uint64)
     _lib.check(g(bt.ctypes.data))
@@ -62,4 +63,6 @@ med["xcd_dur_med_ns"] = [int(x) for x in np.median([r["xcd_dur_med_ns"] for r in
 med["slowest_blocks_last_rep"] = recs[-1]["slowest_blocks"]
 med["slowest_blocks_first_rep"] = recs[a.reps // 4]["slowest_blocks"]
 tiles = [(ntiles - b + 255) // 256 for b in range(min(256, ntiles))]
-print(json.dumps({"rows": a.rows, "nq": a.nq, "tiles_per_block": [min(tiles), max(tiles)], "median": med}, indent=1))
+med["tail_ns_per_rep"] = [r["tail_ns"] for r in recs]
+med["end_max_ns_per_rep"] = [r["end_max_ns"] for r in recs]
+print(json.dumps({"variant": a.variant, "rows": a.rows, "nq": a.nq, "tiles_per_block": [min(tiles), max(tiles)], "median": med}, indent=1))
