@@ -274,10 +274,9 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
   // U1: candidate entries per thread per round (config 3: 512 lists x 10 = 5,120 = one round, rows
   // loaded with the scores, and the drops with them: one memory round trip instead of four).
   // The exact re-score: 16 lanes per survivor row (CPL 16-B chunks of the row per lane), U rows per
-  // 16-lane group in flight: 8 waves x 4 groups x U = 192 rows per round at d 768 (config 3: 94
-  // survivors on average, 214 at most; the 8-GPU shard 75 / 167), so one round, one memory latency,
-  // for nearly every query — the slowest block sets the kernel's time
-  constexpr int NT = 512, NW = NT / 64, CPL = D / 128, U = D == 768 ? 6 : 5, U1 = 10, RPR = NW * 4 * U;
+  // 16-lane group in flight: 8 waves x 4 groups x U = 96 rows per round (config 3: 94 survivors on
+  // average, so one round, one memory latency)
+  constexpr int NT = 512, NW = NT / 64, CPL = D / 128, U = 3, U1 = 10, RPR = NW * 4 * U;
   __shared__ __attribute__((aligned(16))) float ca[kSelCap];  // screen score A of kept candidate i
   __shared__ int crow[kSelCap];   // its row
   __shared__ int srow[kSelCap];   // survivor j's row
