@@ -206,3 +206,41 @@ def test_staged_search_on_two_streams_equals_one_call():
             torch.cuda.synchronize()
             assert torch.equal(out, ref), (nq, mode, blocks)
     ix.enable_screen(1)
+
+
+def test_xcd_balanced_split_is_exact_across_launches_and_streams(rindex):
+    """Kernel 10's XCD-balanced tile split (>= 64 tiles per block: 600k rows) moves tiles between XCDs
+    from launch to launch as the measured speeds change the weights; every launch's answer must be
+    the same (bit for bit) and hold the exact scan's rows, also with two streams searching at once
+    (each launch reads its own weight snapshot)."""
+    n = 600_000
+    ix = rindex.DeviceIndex(768, "bf16")
+    ix.add_synthetic(31, n)
+    q1 = rindex.synth_rows(32, 0, 256, 768, "bf16")
+    q2 = rindex.synth_rows(33, 0, 256, 768, "bf16")
+    ix.enable_screen(0)
+    ex1, ex2 = ix.search(q1, 10), ix.search(q2, 10)
+    ix.enable_screen(1)
+    assert ix.search_plan(256, 10) == 10
+    ref1 = ix.search(q1, 10)
+
+    def same_rows(a, b):  # the exact scan's f32 sums may order an f32 tie differently: compare as sets
+        return torch.equal(torch.sort(a, dim=1)[0], torch.sort(b, dim=1)[0])
+
+    assert same_rows(ref1[1], ex1[1])
+    for _ in range(6):  # the weights move between these launches
+        s, r = ix.search(q1, 10)
+        assert torch.equal(s, ref1[0]) and torch.equal(r, ref1[1])
+    ref2 = ix.search(q2, 10)
+    assert same_rows(ref2[1], ex2[1])
+    sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+    wa = torch.empty(ix.workspace_bytes(256, 10), dtype=torch.uint8, device="cuda")
+    wb = torch.empty_like(wa)
+    torch.cuda.synchronize()
+    outs = []
+    for _ in range(4):
+        outs.append((ix.search(q1, 10, workspace=wa, stream=sa), ix.search(q2, 10, workspace=wb, stream=sb)))
+    torch.cuda.synchronize()
+    for (s1, r1), (s2, r2) in outs:
+        assert torch.equal(s1, ref1[0]) and torch.equal(r1, ref1[1])
+        assert torch.equal(s2, ref2[0]) and torch.equal(r2, ref2[1])
