@@ -3,7 +3,8 @@
 // distance 1, 8 no corpus stream, 16 early slot-table refreshes, 32 slow-path entry count, 64 store-wide
 // integer fast-path bound, 128 epilogue in place, 256 min-of-KL slot bound, 512 slow path never taken,
 // 1024 serial LDS insert, 2048 slow-path issue priority, 4096 static tile split (no XCD balance),
-// 32768 no stage barriers, 65536 per-block start / end wall clocks),
+// 8192 slow-path entries and trips per tile index, 32768 no stage barriers, 65536 per-block start / end
+// wall clocks),
 // via rfx_dbg_screen_variant; variant = 100000 * RING + MODE (RING in {4, 6, 8, 10, 12}).
 #define RFX_K10_BLOCK_TIMES
 #include "k_scan_screen.h"
@@ -57,11 +58,20 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
     RFX_K10V(8, 65536)
     RFX_K10V(8, 4096)
     RFX_K10V(8, 4096 + 65536)
+    RFX_K10V(8, 8192)
     default:
       return -1;
   }
 #undef RFX_K10V
   return 0;
+}
+
+int dbg_k10_trips(unsigned int* out_h, int reset) {
+  if (reset) {
+    static const unsigned int z[2][64] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(k10::g_k10_trips), z, sizeof(z)) == hipSuccess ? 0 : -1;
+  }
+  return hipMemcpyFromSymbol(out_h, HIP_SYMBOL(k10::g_k10_trips), sizeof(k10::g_k10_trips)) == hipSuccess ? 0 : -1;
 }
 
 int dbg_k10_block_times(unsigned long long* out_h) {

@@ -62,6 +62,9 @@ constexpr int kXbWords = 8;  // after the slot table: the XCD split's weight sna
 // debug build only (k10_dbg.hip): MODE 65536 records each block's 100-MHz wall clock when it starts
 // and when all its waves are done (tools/k10_variants.py --block-times)
 __device__ unsigned long long g_k10_bt[1024][2];
+// MODE 8192: per tile index (capped at 63) the wave-tiles that enter the slow path and the pop-loop
+// trips they make (max over the wave's lanes of the passing values), summed over all waves
+__device__ unsigned int g_k10_trips[2][64];
 #endif
 template <int RING>
 constexpr int meta_off() { return RING * kSlot; }
@@ -524,6 +527,19 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
             acc4[2 * rb][i] = (int)r[0];
             acc4[2 * rb + 1][i] = (int)r[1];
           }
+#ifdef RFX_K10_BLOCK_TIMES
+        if constexpr ((MODE & 8192) != 0) {
+          bool pub_;
+          const uint32_t pm_ = fold_mask(acc4, st, lw >> (8 * half), thr, e2, pub_);
+          int c = __popc(pm_);
+#pragma unroll
+          for (int off = 32; off; off >>= 1) c = max(c, __shfl_xor(c, off));
+          if (lane == 0) {
+            atomicAdd(&g_k10_trips[0][it < 63 ? it : 63], 1u);
+            atomicAdd(&g_k10_trips[1][it < 63 ? it : 63], (unsigned)c);
+          }
+        }
+#endif
         fold_screen<KL, (MODE & 1024) == 0>(acc4, st, lw >> (8 * half), Ls, Lr, thr, e2, drop, tile * kTM + 8 * half,
                                             tau_rsrc, slot_voff);
         set_bounds();

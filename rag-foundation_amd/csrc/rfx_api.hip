@@ -1157,6 +1157,7 @@ namespace rfx {
 int dbg_select_times(unsigned long long* out_h);
 int dbg_k11_times(unsigned long long* blocks_h, unsigned long long* last_h);
 int dbg_k10_block_times(unsigned long long* out_h);
+int dbg_k10_trips(unsigned int* out_h, int reset);
 constexpr int k10_tau_words() { return 16; }  // k_scan_screen.h kTauW
 int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, const void* tmv, const uint32_t* sts,
                            int nrows, const int8_t* Qc, const float* qe2, int nq, uint32_t* tau, float* cs, int* cr,
@@ -1276,6 +1277,14 @@ int rfx_dbg_select_times(unsigned long long* out_h) {
 int rfx_dbg_k10_block_times(unsigned long long* out_h) {
   if (!out_h) return fail(RFX_EINVAL, "null out");
   if (rfx::dbg_k10_block_times(out_h) != 0) return fail(RFX_EDEVICE, "hipMemcpyFromSymbol failed");
+  return RFX_OK;
+}
+
+// Diagnostic: kernel 10's slow-path entries and trips per tile index (debug MODE 8192, k10_dbg.hip
+// g_k10_trips [2][64], summed over launches since the last reset; reset != 0 zeroes them).
+int rfx_dbg_k10_trips(unsigned int* out_h, int reset) {
+  if (!out_h && !reset) return fail(RFX_EINVAL, "null out");
+  if (rfx::dbg_k10_trips(out_h, reset) != 0) return fail(RFX_EDEVICE, "hipMemcpy(From|To)Symbol failed");
   return RFX_OK;
 }
 
