@@ -185,16 +185,13 @@ __device__ __forceinline__ void merge_one(const Src& src, int64_t q, int list_le
                                           float* __restrict__ out_s, int64_t* __restrict__ out_r,
                                           MergeRec* __restrict__ out_rec);
 
-// The scan's body, a device function: the kernel below, and kernel 11 (k_screen_valu.hip), whose
-// blocks run it in place when the screen cannot prove its answer (the gated fallback inside the same
-// launch; every block of that launch calls it, so it sees the same grid).
 template <int DT, int NQT, int K, int VPL, bool FUSED>
-__device__ __forceinline__ void scan_valu_body(const uint8_t* __restrict__ X, int nrows, int D,
-                                               const void* __restrict__ Qf, int nq,
-                                               int rows_per_wave, float* __restrict__ cand_s,
-                                               int* __restrict__ cand_r, int n_lists,
-                                               const uint32_t* __restrict__ mask,
-                                               uint32_t* __restrict__ tau, const FusedOut& fo) {
+__global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restrict__ X, int nrows, int D,
+                                                        const void* __restrict__ Qf, int nq,
+                                                        int rows_per_wave, float* __restrict__ cand_s,
+                                                        int* __restrict__ cand_r, int n_lists,
+                                                        const uint32_t* __restrict__ mask,
+                                                        uint32_t* __restrict__ tau, FusedOut fo) {
   if constexpr (FUSED)  // gated (the two-pass scan's fallback): the whole grid returns together
     if (fo.gate && __hip_atomic_load(fo.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
   constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
@@ -442,16 +439,6 @@ __device__ __forceinline__ void scan_valu_body(const uint8_t* __restrict__ X, in
     if (tid < nqt && tau) tau[q0 + tid] = 0u;  // every block's bound updates precede its arrival
     if (tid == 0) fo.ctr[blockIdx.y] = 0u;
   }
-}
-
-template <int DT, int NQT, int K, int VPL, bool FUSED>
-__global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restrict__ X, int nrows, int D,
-                                                        const void* __restrict__ Qf, int nq,
-                                                        int rows_per_wave, float* __restrict__ cand_s,
-                                                        int* __restrict__ cand_r, int n_lists,
-                                                        const uint32_t* __restrict__ mask,
-                                                        uint32_t* __restrict__ tau, FusedOut fo) {
-  scan_valu_body<DT, NQT, K, VPL, FUSED>(X, nrows, D, Qf, nq, rows_per_wave, cand_s, cand_r, n_lists, mask, tau, fo);
 }
 
 // K values instantiated for the scan; runtime k is rounded up to one of these and only the

@@ -86,8 +86,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
                                                           int rows_per_wave, const uint32_t* __restrict__ mask,
                                                           uint32_t* __restrict__ state, float* __restrict__ cand_s,
                                                           int* __restrict__ cand_r, int k_out, float* __restrict__ out_s,
-                                                          int64_t* __restrict__ out_r, int force,
-                                                          uint32_t* __restrict__ vtau, uint32_t* __restrict__ vctr) {
+                                                          int64_t* __restrict__ out_r, int force) {
   constexpr int C = D / 256;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
   const int n_lists = gridDim.x;
@@ -95,32 +94,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   // fallback gate (written by the last block, read by the gated exact search)
   uint32_t* const ctr = state;
   uint32_t* const gate = state + 24;
-  // [32] the launch generation g (read by every block at its start, advanced by the last block), [64] the
-  // last block's verdict for the waiting blocks, 4 g + 1 (proven) or 4 g + 2 (not proven: the exact
-  // fallback runs in this launch).  Nothing to reset: a verdict names its launch (a shared exit
-  // counter measured 5 us at config 2: 249 blocks' atomics on one address).  Each word on a cache line
-  // of its own: the waiting blocks poll the verdict, and polling the arrival counter's line slowed
-  // every block's arrival (block record + arrival 2.1 -> 3.9 us median).
-  uint32_t* const genw = state + 32;
-  uint32_t* const dec = state + 64;
-  // The exact fallback in place (the one-launch VALU search's body, k_scan_valu.h): every block of this
-  // launch runs it when the last block could not prove the answer; its final top-k re-scored by the
-  // two-pass rule.  Dynamic LDS: its staged queries.
-  constexpr int ESZV = DT == RFX_F32 ? 4 : 2;
-  constexpr int VPR0 = D * ESZV / 16;
-  constexpr int VPLV = (VPR0 + 15) / 16 <= 4 ? 4 : (VPR0 + 15) / 16 <= 8 ? 8 : (VPR0 + 15) / 16 <= 12 ? 12 : 16;
-  // in place for a lone question (config 2's case) where the two bodies fit the register file together;
-  // otherwise (several questions, f32 at d 1024: spills) the host launches the gated fallback after it
-  constexpr bool INL = screen_valu_inline_fallback(NQT, DT, D);
-  auto fallback = [&]() {
-    if constexpr (INL)
-      scan_valu_body<DT, NQT, 16, VPLV, true>((const uint8_t*)X, nrows, D, Q, nq, rows_per_wave, cand_s, cand_r,
-                                              gridDim.x, mask, vtau, FusedOut{vctr, k_out, out_s, out_r, gate});
-  };
   RFX_K11_T(0);
-  // (every block reads the generation before it arrives; the last block advances it only after every
-  // block has arrived)
-  const uint32_t gen0 = INL ? __hip_atomic_load(genw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
 
   // The int8 row stream (step 2): iteration t scores rows wb + 64 (t >> 4) + 4 (t & 15) + g.  Its first
   // NB - 1 iterations of loads are issued here, before the query quantiser, so their latency overlaps
@@ -360,33 +334,12 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   }
   __syncthreads();
   RFX_K11_T(3);
-  if (!INL && !last) return;
-  if (!last) {
-    // wait for the last block's verdict on this launch (bounded: a lost verdict ends the wait, it never
-    // hangs the grid)
-    __shared__ uint32_t verdict;
-    if (tid == 0) {
-      uint32_t d = 0u;
-      for (int it = 0; it < (1 << 22); ++it) {
-        d = __hip_atomic_load(dec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((d >> 2) == (gen0 & 0x3fffffffu) && (d & 3u)) break;
-        __builtin_amdgcn_s_sleep(8);
-      }
-      verdict = (d >> 2) == (gen0 & 0x3fffffffu) ? (d & 3u) : 0u;
-    }
-    __syncthreads();
-    if (verdict == 2u) fallback();
-    return;
-  }
+  if (!last) return;
   RFX_K11_L(0);
   if (force & 8) {
     if (tid == 0) {
       *gate = 0u;
       *ctr = 0u;
-      if (INL && gridDim.x > 1) {
-        __hip_atomic_store(dec, ((gen0 & 0x3fffffffu) << 2) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(genw, gen0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
     }
     return;
   }
@@ -575,19 +528,9 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     if (qi == 0) RFX_K11_L(4);
   }
   RFX_K11_L(5);
-  const bool fb = fail != 0;
   if (tid == 0) {
-    __hip_atomic_store(gate, fb ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the gate is visible before the verdict
-    if (INL && gridDim.x > 1) {
-      __hip_atomic_store(dec, ((gen0 & 0x3fffffffu) << 2) | (fb ? 2u : 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(genw, gen0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    *gate = fail ? 1u : 0u;  // read by the gated exact search that follows on the stream
     *ctr = 0u;
-  }
-  if (INL && fb) {
-    __syncthreads();
-    fallback();
   }
 }
 
@@ -600,23 +543,16 @@ int dbg_k11_times(unsigned long long* blocks_h, unsigned long long* last_h) {
 }
 #endif
 
-// One launch: grid (blocks) × 256 threads, one query slice of up to 8 queries.  The exact fallback
-// runs inside it (k 5..16: the VALU scan's K slot 16); dynamic LDS = its staged queries [NQT][D] f32.
-// state: kernel 11's words; vstate: the one-launch VALU search's (bounds, then counters).
+// One launch: grid (blocks) × 256 threads, one query slice of up to 8 queries.
 int launch_screen_valu(const ValuPlan& p, const int8_t* X8, const void* tmeta, const uint32_t* stats, int nrows, int D,
                        int dtype, const void* X, const void* Q, int nq, const uint32_t* mask, uint32_t* state,
-                       uint32_t* vstate, float* cs, int* cr, int k, float* out_s, int64_t* out_r, int force,
-                       hipStream_t st) {
-  if (nq < 1 || nq > 8 || k < 5 || k > kK || (D != 768 && D != 1024) || !vstate) return -1;
-  if ((int64_t)p.blocks * kK > (int64_t)1 << 30 || p.q_slices != 1 || valu_k_slot(k) != 16) return -1;
+                       float* cs, int* cr, int k, float* out_s, int64_t* out_r, int force, hipStream_t st) {
+  if (nq < 1 || nq > 8 || k < 1 || k > kK || (D != 768 && D != 1024)) return -1;
+  if ((int64_t)p.blocks * kK > (int64_t)1 << 30) return -1;
   const dim3 grid((unsigned)p.blocks);
-  uint32_t* const vtau = vstate;
-  uint32_t* const vctr = vstate + kValuFusedMaxNq;
 #define RFX_SV(DTV, DV, NQ)                                                                                      \
-  hipLaunchKernelGGL((screen_valu_kernel<DTV, DV, NQ>), grid, dim3(256),                                          \
-                     screen_valu_inline_fallback(NQ, DTV, DV) ? (size_t)(NQ) * (DV) * sizeof(float) : 0, st,     \
-                     X8, (const uint4*)tmeta, stats, nrows, X, Q, nq, p.rows_per_wave, mask, state, cs, cr, k, out_s, \
-                     out_r, force, vtau, vctr)
+  hipLaunchKernelGGL((screen_valu_kernel<DTV, DV, NQ>), grid, dim3(256), 0, st, X8, (const uint4*)tmeta, stats, nrows, \
+                     X, Q, nq, p.rows_per_wave, mask, state, cs, cr, k, out_s, out_r, force)
 #define RFX_SV_D(DTV)                  \
   if (D == 768) {                      \
     if (nq == 1)                       \

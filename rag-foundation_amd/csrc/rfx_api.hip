@@ -1363,24 +1363,19 @@ int search_impl(rfx_index_t h, const void* queries_d, int64_t nq, int k, const u
   };
   if ((!pack || L.pk_off) && screen_valu_eligible(*ix, L, nq, k) && ((uintptr_t)queries_d & 15) == 0) {
     uint32_t* state = nullptr;
-    std::unique_lock<std::mutex> slk(ix->state_mu);  // held until the launches are enqueued
+    std::unique_lock<std::mutex> slk(ix->state_mu);  // held until both launches are enqueued
     if ((rc = fused_state(*ix, st, &state, slk))) return rc;
     uint32_t* sv = state + rfx::kScreenValuState;
     if ((rc = mark(ev0))) return rc;
-    // one launch: the screen, and the exact one-launch search run by the same blocks when the screen
-    // cannot prove its answer (its state: the front of the same per-stream search state)
     if (rfx::launch_screen_valu(L.vp, ix->scodes, ix->smeta, ix->sstats, (int)ix->rows, ix->dim, ix->dtype, ix->data,
-                                queries_d, (int)nq, row_mask_d, sv, state, cs, cr, k, vo_s, vo_r,
+                                queries_d, (int)nq, row_mask_d, sv, cs, cr, k, vo_s, vo_r,
                                 (ix->screen == 2 ? 1 : 0) | k11_ablate(), st) != 0)
       return fail(RFX_EUNSUPPORTED, "two-pass VALU search launch rejected");
     if ((rc = mark(ev1))) return rc;
-    if (!rfx::screen_valu_inline_fallback(nq == 1 ? 1 : 8, ix->dtype, ix->dim)) {
-      // several questions (or f32 rows at d 1024): the exact one-launch search, gated on the word the
-      // screen's last block wrote
-      if (rfx::launch_search_valu_fused(L.vp, ix->data, (int)ix->rows, ix->dim, ix->dtype, queries_d, (int)nq, cs,
-                                        cr, state, k, vo_s, vo_r, st, row_mask_d, sv + 24) != 0)
-        return fail(RFX_EUNSUPPORTED, "VALU search launch rejected");
-    }
+    // the exact one-launch search, gated on the word the screen's last block wrote
+    if (rfx::launch_search_valu_fused(L.vp, ix->data, (int)ix->rows, ix->dim, ix->dtype, queries_d, (int)nq, cs, cr,
+                                      state, k, vo_s, vo_r, st, row_mask_d, sv + 24) != 0)
+      return fail(RFX_EUNSUPPORTED, "VALU search launch rejected");
     RFX_HIP(hipGetLastError());
     slk.unlock();
     return finish_pack();

@@ -55,20 +55,10 @@ int launch_search_valu_fused(const ValuPlan& p, const void* X, int nrows, int D,
 // Kernel 11 (k_screen_valu.hip): the exact two-pass scan of nq <= 8 questions in one launch over the
 // index's int8 copy (codes X8, tile records tmeta, quantiser stats), the exact rows X / queries Q in
 // the index dtype; writes (out_s, out_r) and the fallback gate state[24] (state = the index's
-// per-stream search state + kScreenValuState, zero on entry and left zero except the gate).  When the
-// screen cannot prove its answer, every block runs the exact one-launch VALU search in the same launch
-// (vstate = that search's state: bounds, then counters; the search state's base), so no gated launch
-// follows.  5 <= k <= 16, one query slice.
+// per-stream search state + kScreenValuState, zero on entry and left zero except the gate).
 int launch_screen_valu(const ValuPlan& p, const int8_t* X8, const void* tmeta, const uint32_t* stats, int nrows, int D,
                        int dtype, const void* X, const void* Q, int nq, const uint32_t* mask, uint32_t* state,
-                       uint32_t* vstate, float* cs, int* cr, int k, float* out_s, int64_t* out_r, int force,
-                       hipStream_t st);
-// Kernel 11 runs the exact fallback inside its own launch for a lone question (NQT 1) except f32 rows
-// at d 1024 (the two bodies together would spill); otherwise the caller launches the gated one-launch
-// VALU search after it (launch_search_valu_fused with gate = state + 24).
-constexpr bool screen_valu_inline_fallback(int nqt, int dtype, int D) {
-  return nqt == 1 && !(dtype == RFX_F32 && D == 1024);
-}
+                       float* cs, int* cr, int k, float* out_s, int64_t* out_r, int force, hipStream_t st);
 
 // ---- MFMA scan (batched bf16 / f16) -------------------------------------------------------
 struct MfmaPlan {
