@@ -15,7 +15,9 @@ Quantiser (per 32-row tile; dead rows = any NaN element: code 0, live bit clear)
     stats = (max ||x||, max ||x - s_t c||) over live rows, rounded up to f32, and max s_t (the
             screen kernel's fast-path bound: no per-tile data on the fast path).
 Queries: s_y, c_y likewise per query; E_q = Xmax ||y - s_y c_y|| + Emax ||s_y c_y|| (Cauchy-Schwarz);
-    e2 = (2 E_q + 4e-7 (Xmax + Emax) ||s_y c_y||) (1 + 1e-5) / s_y, rounded up to f32.
+    e2 = (2 E_q + 4e-7 (Xmax + Emax) ||s_y c_y|| + 2.4e-7 Xmax (||s_y c_y|| + ||y - s_y c_y||)) (1 + 1e-5) / s_y,
+    rounded up to f32 (the 2.4e-7 term: two f32 ulps of the k-th exact score, so a row whose exact
+    score rounds to the k-th's f32 with a smaller row id survives under the score rule).
 Screen score (units of s_y): A = f32(c_x . c_y) * s_t (one f32 rounding).  Survivors of a query:
 rows with A >= a_k - e2 (a_k = k-th best A over live rows); exact re-score; top-k.
 """
@@ -81,7 +83,8 @@ def quantize_queries(q32, stats):
     xm, em = float(stats[0]), float(stats[1])
     eq = xm * ey + em * yh
     with np.errstate(divide="ignore", invalid="ignore"):
-        e2 = np.where(s > 0, (2.0 * eq + 4e-7 * (xm + em) * yh) * (1.0 + 1e-5) / s.astype(np.float64), 0.0)
+        e2 = np.where(s > 0, (2.0 * eq + 4e-7 * (xm + em) * yh + 2.4e-7 * xm * (yh + ey)) * (1.0 + 1e-5)
+                      / s.astype(np.float64), 0.0)
     return c, _f32_up(e2), s
 
 

@@ -5,7 +5,10 @@
 // 1024 serial LDS insert, 2048 slow-path issue priority, 4096 static tile split (no XCD balance),
 // 8192 slow-path entries and trips per tile index, 32768 no stage barriers, 65536 per-block start / end
 // wall clocks),
-// via rfx_dbg_screen_variant; variant = 100000 * RING + MODE (RING in {4, 6, 8, 10, 12}).
+// 131072 epilogue after the stage-0 barrier, 262144 waves 4-7 one stage later (stagger), 524288 partner
+// bound by v_permlane16_swap (round 5),
+// via rfx_dbg_screen_variant; variant = 10^7 * RING + MODE (RING in {4, 6, 8, 10, 12}; rounds 3-4 used
+// 100000 * RING + MODE).
 #define RFX_K10_BLOCK_TIMES
 #include "k_scan_screen.h"
 
@@ -19,7 +22,7 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
   const int ntiles = (nrows + k10::kTM - 1) / k10::kTM;
   dim3 grid(p.blocks, p.q_blocks);
 #define RFX_K10V(R, M)                                                                                        \
-  case 100000 * R + M:                                                                                          \
+  case 10000000 * R + M:                                                                                          \
     hipLaunchKernelGGL((k10::scan_screen_kernel<10, 768, false, R, M>), grid, dim3(512), 0, st, X, tm, sts, Qc, \
                        qe2, nq, ntiles, tau, cs, cr, dr, p.n_lists, nullptr, tau + p.nq_pad * k10::kTauW,      \
                        xcd_weights_device_ptr());                                                             \
@@ -59,6 +62,14 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
     RFX_K10V(8, 4096)
     RFX_K10V(8, 4096 + 65536)
     RFX_K10V(8, 8192)
+    RFX_K10V(8, 131072)
+    RFX_K10V(8, 262144)
+    RFX_K10V(8, 393216)
+    RFX_K10V(8, 524288)
+    RFX_K10V(8, 655360)
+    RFX_K10V(8, 917504)
+    RFX_K10V(8, 131072 + 8192)
+    RFX_K10V(8, 393216 + 8192)
     default:
       return -1;
   }

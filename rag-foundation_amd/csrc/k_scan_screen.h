@@ -275,6 +275,10 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
 // 1024 = the slow path's serial LDS list insert instead of the register-resident list, 16 = the slot
 // table re-read at every one of the first 16 tiles, 2048 = issue priority for a wave in the slow path,
 // 32768 = the ring without stage barriers (DEC below).
+// debug MODE bits of round 5 (k10_dbg.hip; variant = 10^7 * RING + MODE)
+constexpr int kModeEpiLate = 131072;
+constexpr int kModeStagger = 262144;
+constexpr int kModePermBounds = 524288;
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
@@ -419,16 +423,23 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   // the store-wide smax bound it skips the tiles whose scale lies below smax (measured: 17 % of
   // wave-tiles entered the slow path with the smax bound).
   float tf_own = -__builtin_inff(), tf_oth = -__builtin_inff();
+  const bool odd = ((lane >> 4) & 1) != 0;
   auto set_bounds = [&]() {
     if constexpr ((MODE & 64) != 0) {
       ti_own = ibound(thr);
       ti_oth = __shfl_xor(ti_own, 16);
     } else {
       tf_own = thr ? unord(thr) - e2 : -__builtin_inff();
-      tf_oth = __shfl_xor(tf_own, 16);
+      if constexpr ((MODE & kModePermBounds) != 0) {
+        // the partner lane's (lane ^ 16) bound by one v_permlane16_swap: no ds_bpermute round trip
+        const uint32_t b = __float_as_uint(tf_own);
+        const auto r = __builtin_amdgcn_permlane16_swap(b, b, false, false);
+        tf_oth = __uint_as_float(odd ? r[0] : r[1]);
+      } else {
+        tf_oth = __shfl_xor(tf_own, 16);
+      }
     }
   };
-  const bool odd = ((lane >> 4) & 1) != 0;
   // MODE 32 (debug) counts slow-path entries in slot 15 of each wave's first query: 15 slots then;
   // MODE 256 (debug): kernel 6's bound, the min over KL slots (list j -> slot j % KL)
   constexpr int kSlots = (MODE & 256) != 0 ? KL : (MODE & 32) != 0 ? kTauW - 1 : kTauW;
@@ -627,8 +638,22 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
           for (int qb = 0; qb < 2; ++qb)
             acc4[2 * rb + qb] = ks == 0 ? mfma_i8(cur.a[rb], bq[2 * ks + qb], v4i32{0, 0, 0, 0})
                                         : mfma_i8(cur.a[rb], bq[2 * ks + qb], acc4[2 * rb + qb]);
-        if constexpr ((MODE & 128) == 0)
-          if (s == 0 && kk == 0 && prev) epilogue(it - 1, accp);
+        if constexpr ((MODE & 128) == 0) {
+          // where the epilogue of tile it - 1 runs inside tile it (its accumulators stay live until tile
+          // it + 1's first k-step): production right after k-step 0 (before stage 0's barrier); debug
+          // kModeEpiLate after the MFMAs of the barrier's k-step (a wave in the slow path then has a whole
+          // stage of k-steps before the next barrier); kModeStagger: waves 4-7 (the SIMD partners of waves
+          // 0-3) one stage later, so the two waves of a SIMD do not run their VALU epilogues together
+          constexpr int EK = (MODE & kModeEpiLate) != 0 ? KB : 0;
+          if (kk == EK && prev) {
+            if constexpr ((MODE & kModeStagger) != 0 && NST >= 2) {
+              if (s == 0 && w < 4) epilogue(it - 1, accp);
+              if (s == 1 && w >= 4) epilogue(it - 1, accp);
+            } else {
+              if (s == 0) epilogue(it - 1, accp);
+            }
+          }
+        }
       }
     }
 

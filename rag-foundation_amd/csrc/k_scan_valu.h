@@ -105,11 +105,15 @@ struct FusedOut {
   const uint32_t* gate = nullptr;
 };
 
-// The two-pass scan's score rule: a returned score is fl32(exact dot), the f64 sum of the exact
-// products rounded once, and the order is (that f32 score desc, row asc) — what kernel 10's select and
-// kernel 11's last block return.  When either falls back to an exact scan (f32 accumulation), the
-// fallback's final top-k is re-scored by the same rule (`Rescore`), so an answer's bits do not depend
-// on which path a query (or a shard of a sharded store) took.
+// The score rule of every search (round 5: one rule for every plan): a returned score is fl32(exact
+// dot), the f64 sum of the exact products rounded once, and the order is (that f32 score desc, row asc)
+// — what kernel 10's select and kernel 11's last block return.  The exact scans (f32 accumulation:
+// kernels 1-3, 6, 8, 9, VALU) pick their final top-k by their own sums and that top-k is then
+// re-scored and re-ordered by the same rule (`Rescore`: here in the one-launch VALU search, and in the
+// merge of every other exact plan and of the two-pass scan's gated fallback), so an answer's bits do
+// not depend on which path a query (or a shard of a sharded store) took.  (The SET can differ from the
+// two-pass scan's only where two rows' exact scores lie within the f32 accumulation error of each other
+// at the k-th place)
 // (struct Rescore: rfx_kernels.h)
 
 __device__ __forceinline__ float elem_rt(const void* p, int64_t i, int dtype) {
@@ -119,8 +123,9 @@ __device__ __forceinline__ float elem_rt(const void* p, int64_t i, int dtype) {
 }
 
 // Block-wide (any block size that is a multiple of 64, k_out <= 64): the k_out entries just written
-// for query q (out_s / out_r, or out_rec with row_offset added) re-scored and re-ordered by the rule
-// above.  The caller's writes are read back with agent-scope loads after a barrier.
+// for query q (out_s / out_r, or out_rec; the merge added row_offset to the rows in both forms, so the
+// row of X is row - row_offset either way) re-scored and re-ordered by the rule above.  The caller's
+// writes are read back with agent-scope loads after a barrier.
 __device__ __forceinline__ void rescore_final(const Rescore& rs, int64_t q, int k_out, int64_t row_offset,
                                               float* out_s, int64_t* out_r, MergeRec* out_rec) {
   __shared__ float rs_s[64];
@@ -140,7 +145,7 @@ __device__ __forceinline__ void rescore_final(const Rescore& rs, int64_t q, int 
     }
     double acc = 0.0;
     if (row >= 0) {
-      const int64_t xr = (row - (out_rec ? row_offset : 0)) * rs.D, qr = q * rs.D;
+      const int64_t xr = (row - row_offset) * rs.D, qr = q * rs.D;
       for (int c = gl; c < rs.D; c += 8)
         acc += (double)elem_rt(rs.X, xr + c, rs.dtype) * (double)elem_rt(rs.Q, qr + c, rs.dtype);
     }
@@ -426,14 +431,14 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
         __syncthreads();
         merge_one<K, false, 4, true>(lsrc, q0 + qi, K, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
         __syncthreads();
-        if (fo.gate) rescore_final(Rescore{X, Qf, D, DT}, q0 + qi, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
+        rescore_final(Rescore{X, Qf, D, DT}, q0 + qi, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
       }
     } else {
       const AgentSrc src{cand_s, cand_r, n};
       for (int qi = 0; qi < nqt; ++qi) {
         merge_one<K, false, 4, true>(src, q0 + qi, K, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
         __syncthreads();
-        if (fo.gate) rescore_final(Rescore{X, Qf, D, DT}, q0 + qi, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
+        rescore_final(Rescore{X, Qf, D, DT}, q0 + qi, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
       }
     }
     if (tid < nqt && tau) tau[q0 + tid] = 0u;  // every block's bound updates precede its arrival

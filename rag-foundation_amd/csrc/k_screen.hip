@@ -151,9 +151,12 @@ __global__ __launch_bounds__(256) void screen_quantize_kernel(const void* __rest
 
 // ---- per batch: query codes and e2 (one wave per query) -------------------------------------------
 // s_y = amax / 127, c = clamp(rint(y / s_y)); E_q = Xmax ||y − s_y c|| + Emax ||s_y c|| (Cauchy-Schwarz,
-// k_scan_screen.h); e2 = (2 E_q + 4e-7 (Xmax + Emax) ||s_y c||) (1 + 1e-5) / s_y rounded up: the
-// 4e-7 term covers the f32 roundings of A = s_t D (2^-24 relative, twice) and of the bound
-// subtraction, the 1e-5 the f64 norms.  Also zeroes the query's threshold slots and (block 0) the
+// k_scan_screen.h); e2 = (2 E_q + 4e-7 (Xmax + Emax) ||s_y c|| + 2.4e-7 Xmax (||s_y c|| + ||y - s_y c||))
+// (1 + 1e-5) / s_y rounded up: the 4e-7 term covers the f32 roundings of A = s_t D (2^-24 relative,
+// twice) and of the bound subtraction, the 2.4e-7 term two f32 ulps of the k-th exact score (>= 2^-23
+// |score|, |score| <= Xmax ||y||): under the score rule (fl32 of the exact dot desc, row asc) a row
+// whose exact score is below the k-th but rounds to the same f32 and has a smaller row id belongs to
+// the answer, so it must survive; the 1e-5 the f64 norms.  Also zeroes the query's threshold slots and (block 0) the
 // fallback gate.  Padded queries (q >= nq) get code 0 and e2 0.
 // Kernel 10's XCD table, one per device (k_scan_screen.h: the tile split across the 8 XCDs): [0, 8)
 // weights (1024 = 1.0, 0 = not measured yet), [8, 16) the blocks' durations (10-ns ticks) and [16, 24)
@@ -242,7 +245,7 @@ __global__ __launch_bounds__(256) void screen_queries_kernel(const uint16_t* __r
       const double xm = (double)__uint_as_float(stats[0]), em = (double)__uint_as_float(stats[1]);
       const double yh = (double)s * sqrt((double)cc);
       const double eq = xm * sqrt(ey) + em * yh;
-      e2 = f32_up((2.0 * eq + 4e-7 * (xm + em) * yh) * (1.0 + 1e-5) / (double)s);
+      e2 = f32_up((2.0 * eq + 4e-7 * (xm + em) * yh + 2.4e-7 * xm * (yh + sqrt(ey))) * (1.0 + 1e-5) / (double)s);
     }
     qe2[q] = e2;
   }

@@ -166,7 +166,8 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     if (lane == 0) {
       const double yh = (double)s * sqrt((double)cc);
       const double eq = xm * sqrt(ey) + em * yh;
-      const float e2 = f32_up((2.0 * eq + 4e-7 * (xm + em) * yh) * (1.0 + 1e-5) / (double)sd);
+      const float e2 = f32_up((2.0 * eq + 4e-7 * (xm + em) * yh + 2.4e-7 * xm * (yh + sqrt(ey))) * (1.0 + 1e-5) /
+                              (double)sd);  // (the e2 rule of k_screen.hip)
       e2_lds[qi] = s > 0.f ? e2 : 0.f;
     }
   };

@@ -1407,9 +1407,12 @@ int search_impl(rfx_index_t h, const void* queries_d, int64_t nq, int k, const u
     if (rc) return rc;
     if ((rc = mark(ev1))) return rc;
   }
-  // the scan's candidates are sorted lists: the merge bounds admission by the lists' k-th entries
+  // the scan's candidates are sorted lists: the merge bounds admission by the lists' k-th entries; its
+  // final top-k is re-scored by the score rule of every plan (fl32 of the f64 dot; k_scan_valu.h)
+  const rfx::Rescore rs{ix->data, queries_d, ix->dim, ix->dtype};
   if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, n_cand, list_len, k, row_offset, out_rec ? nullptr : out_scores_d,
-                                   out_rec ? nullptr : out_rows_d, out_rec, st, /*sorted=*/n_cand > 0) != 0)
+                                   out_rec ? nullptr : out_rows_d, out_rec, st, /*sorted=*/n_cand > 0, nullptr,
+                                   n_cand > 0 ? &rs : nullptr) != 0)
     return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
   RFX_HIP(hipGetLastError());
   return RFX_OK;

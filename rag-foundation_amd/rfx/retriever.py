@@ -55,28 +55,42 @@ def union_budget() -> int:
     return int(os.environ.get("RFX_UNION_MAX_BYTES", str(32 << 30)))
 
 
-def _evict_union(key):
-    """(caller holds _STATE_LOCK)"""
+def _evict_union(key, closing):
+    """(caller holds _STATE_LOCK) Drop the view from the cache; an unpinned view goes to `closing`, which the
+    caller closes after releasing the lock.  Its bytes stay counted until it is closed (a pinned view's
+    device memory lives until its last user releases it: ADVICE r4)."""
     v = _UNIONS.pop(key)
-    _UNION_BYTES[0] -= v.nbytes
     v.evicted = True
     if v.users == 0:
+        closing.append(v)
+
+
+def _close_unions(closing):
+    """Close evicted views outside _STATE_LOCK (hipFree may wait for the device), then uncount them."""
+    for v in closing:
         v.close()
+    if closing:
+        with _STATE_LOCK:
+            _UNION_BYTES[0] -= sum(v.nbytes for v in closing)
 
 
 def _release_union(v):
+    closing = []
     with _STATE_LOCK:
         v.users -= 1
         if v.evicted and v.users == 0:
-            v.close()
+            closing.append(v)
+    _close_unions(closing)
 
 
 def _purge_batchers(name):
+    closing = []
     with _STATE_LOCK:
         for key in [k for k in _BATCHERS if k[0] == name or (isinstance(k[0], tuple) and name in k[0])]:
             del _BATCHERS[key]
         for key in [k for k in _UNIONS if name in k[0]]:
-            _evict_union(key)
+            _evict_union(key, closing)
+    _close_unions(closing)
 
 
 class GpuRetriever:
@@ -184,29 +198,62 @@ class GpuRetriever:
     def _union_view(self, names, stores):
         """The cached view over `stores` brought up to date (in place when the members only grew or
         deleted rows), pinned for the caller (_release_union), or None when a view of this size does not
-        fit the cache's byte budget.  Callers hold every member's lock."""
+        fit the cache's byte budget.  Callers hold every member's lock.
+
+        The device copies (a view's build, a follow's appended rows) run OUTSIDE _STATE_LOCK (VERDICT r4
+        #7): that lock guards the cache's dict and counters only, and every batcher, embedder and union
+        lookup of the process takes it, so a copy under it would stall every chat thread.  What serialises
+        the copies is the member locks the caller holds: every user of a view holds all of its members'
+        locks (the key is the member list), so no other thread searches or follows this view meanwhile."""
         key = (tuple(names), id(self.registry))
         want = runion.union_key(stores)
+        closing = []
         with _STATE_LOCK:
             v = _UNIONS.get(key)
             if v is not None:
                 _UNIONS.move_to_end(key)
-                if v.key == want or v.follow(stores):
-                    v.users += 1
-                    return v
-                _evict_union(key)
-            need, budget = runion.planned_bytes(stores), union_budget()
-            if need > budget:
-                return None
+                v.users += 1  # pinned: an eviction meanwhile leaves it open for us
+        if v is not None:
+            ok = v.key == want
+            if not ok:
+                try:
+                    ok = v.follow(stores)
+                except BaseException:
+                    _release_union(v)
+                    raise
+            if ok:
+                return v
+            with _STATE_LOCK:
+                if _UNIONS.get(key) is v:
+                    _evict_union(key, closing)
+            _release_union(v)
+        _close_unions(closing)
+        closing = []
+        need, budget = runion.planned_bytes(stores), union_budget()
+        if need > budget:
+            return None
+        with _STATE_LOCK:  # room for it (bytes reserved while it is built)
             while _UNIONS and _UNION_BYTES[0] + need > budget:
-                _evict_union(next(iter(_UNIONS)))
+                _evict_union(next(iter(_UNIONS)), closing)
+            _UNION_BYTES[0] += need
             if self.registry.on_evict.count(_purge_batchers) == 0:
                 self.registry.on_evict.append(_purge_batchers)
+        _close_unions(closing)
+        closing = []
+        try:
             v = runion.UnionView(stores)
-            v.users, v.evicted = 1, False
+        except BaseException:
+            with _STATE_LOCK:
+                _UNION_BYTES[0] -= need
+            raise
+        v.users, v.evicted = 1, False
+        with _STATE_LOCK:
+            _UNION_BYTES[0] += v.nbytes - need
+            if key in _UNIONS:  # (cannot happen while the caller holds the member locks; stay consistent)
+                _evict_union(key, closing)
             _UNIONS[key] = v
-            _UNION_BYTES[0] += v.nbytes
-            return v
+        _close_unions(closing)
+        return v
 
     def _run_union_batch(self, names, metadata_filter, items):
         """Batch runner over a store list: one embedding GEMM, one scan + merge of the members'

@@ -53,6 +53,7 @@ class ShardedIndex:
         self._split = False
         self.generation = 0  # bumped whenever the shard layout changes (ShardedIvf rebuilds its lists)
         self._screen = 0     # the two-pass scan's int8 copies (enable_screen), re-made on new shards
+        self.screen_dropped = False  # a shard's copy was dropped by growth: every shard went exact
         self._tombs = []  # tombstoned global rows (re-applied after a re-split)
         distinct = len(set(self.devices)) == len(self.devices)
         self.comm = RcclComm.for_devices(self.devices) if distinct and len(self.devices) > 1 else None
@@ -105,6 +106,7 @@ class ShardedIndex:
             return
         last = self.shards[-1]
         last.rows_sync(path, upto - self.bases[-1], file_base=self.bases[-1])
+        self._screen_follow()
         others = [s.rows for s in self.shards[:-1]]
         if others and last.rows > 2 * max(1.0, sum(others) / len(others)) and upto >= 64 * ALIGN * len(self.shards):
             self._resplit(path, upto)
@@ -152,6 +154,8 @@ class ShardedIndex:
                 for sh in new:
                     sh.enable_screen(0)
                 self._screen = 0
+                self.screen_dropped = True
+            self._screen_follow()  # (shard 0 appended its new tail: its copy may have been dropped)
 
     def add(self, vecs: torch.Tensor) -> int:
         """Append rows (writer path): they extend the last shard."""
@@ -160,7 +164,29 @@ class ShardedIndex:
             self._split = True
             last = self.shards[-1]
             last.add(vecs.to(torch.device("cuda", self.devices[-1])))
+            self._screen_follow()
             return first
+
+    def _screen_follow(self) -> None:
+        """All or nothing after growth: only the last shard takes appends, and librfx drops
+        a shard's int8 copy when an append outgrows the room the copy has (rfx_index_screen_state reports
+        it).  Then every shard drops its copy, so every shard answers with the exact plan (the same score
+        rule either way, but one plan per store)."""
+        if not self._screen:
+            return
+        if any(sh.screen_state()[0] == 0 for sh in self.shards):
+            for sh in self.shards:
+                sh.enable_screen(0)
+            self._screen = 0
+            self.screen_dropped = True
+
+    def screen_state(self):
+        """(mode, device bytes of the shards' int8 copies, dropped) — DeviceIndex.screen_state over the
+        shards: mode is the store's (0 once any shard lost its copy), dropped = a copy was dropped by
+        growth since enable_screen."""
+        states = [sh.screen_state() for sh in self.shards]
+        mode = self._screen if all(m for m, _, _ in states) else 0
+        return mode, sum(b for _, b, _ in states), bool(self.screen_dropped or any(d for _, _, d in states))
 
     def rows_append(self, path: str, row0: int) -> None:
         """Write global rows [row0, rows) to the row file, shard by shard in row order."""
@@ -281,6 +307,8 @@ class ShardedIndex:
                 self._screen = 0
                 raise
             self._screen = int(mode)
+            if mode:
+                self.screen_dropped = False
 
     # ---- IVF (config 5) --------------------------------------------------------------------------
     def new_ivf(self, nlist):

@@ -45,13 +45,19 @@ def planned_rows(stores) -> int:
     return sum(_region(st.index.rows) for st in stores)
 
 
+def members_screened(stores) -> bool:
+    """The view keeps an int8 copy (and answers with the two-pass scan) when every member does: each
+    member's state as it stands (LocalStore._screen_on follows a copy that growth dropped),
+    not the first member's.  Either plan returns the same bits (one score rule, k_scan_valu.h)."""
+    return all(getattr(st, "_screen_on", False) is True for st in stores)
+
+
 def planned_bytes(stores) -> int:
     """Device bytes a view over `stores` would hold: the rows, and the int8 copy when the members
     answer with the two-pass scan (dim bytes per row)."""
     st0 = stores[0]
     n = planned_rows(stores)
-    screened = getattr(st0, "_screen_on", False) is True
-    return n * st0.dim * (ESIZE[st0.dtype] + (1 if screened else 0))
+    return n * st0.dim * (ESIZE[st0.dtype] + (1 if members_screened(stores) else 0))
 
 
 def eligible(stores) -> bool:
@@ -74,7 +80,7 @@ class UnionView:
         self.gens = [st.generation for st in stores]
         st0 = stores[0]
         self.dim, self.dtype, self.device = st0.dim, st0.dtype, st0.device
-        self.screened = getattr(st0, "_screen_on", False) is True
+        self.screened = members_screened(stores)
         self.bases, self.rows, self.regions, self.tombs = [], [], [], []
         self.rows_copied = 0  # rows this view copied from its members (tests / profiles: O(appended))
         self.users, self.evicted = 0, False  # pins of the retriever's view cache (rfx.retriever)
@@ -120,7 +126,7 @@ class UnionView:
         headroom, a member that shrank): then the caller rebuilds the view."""
         if [st.name for st in stores] != self.names or [st.generation for st in stores] != self.gens:
             return False
-        if (getattr(stores[0], "_screen_on", False) is True) != self.screened:
+        if members_screened(stores) != self.screened:
             return False
         for st, n0, reg, t0 in zip(stores, self.rows, self.regions, self.tombs):
             if st.index.rows < n0 or st.index.rows > reg or st.tombs < t0:

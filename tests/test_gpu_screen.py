@@ -163,6 +163,30 @@ def test_search_records_row_offset(rindex):
     assert np.array_equal((rec[..., 0] & 0xffffffff).astype(np.uint32).view(np.float32), s.cpu().numpy())
 
 
+@pytest.mark.parametrize("mode", [1, 2])
+def test_scores_rows_form_with_row_offset_equals_records(rindex, mode):
+    """rfx_search_timed writing (scores, rows) with a row offset — through the select, and through the
+    forced gated fallback (mode 2), whose merge adds the offset and whose re-score must subtract it
+    again before it reads the shard's rows — equals the records form."""
+    from rfx._lib import check, lib, ptr, stream_ptr
+
+    ix, _ = _make(rindex, 9000, 768, "bf16", screen=mode)
+    q, _ = _queries(rindex, 256, 768, "bf16")
+    off = 1000
+    rec = ix.search_records(q, 10, row_offset=off)
+    ws = torch.empty(ix.workspace_bytes(256, 10), dtype=torch.uint8, device="cuda")
+    s = torch.empty((256, 10), dtype=torch.float32, device="cuda")
+    r = torch.empty((256, 10), dtype=torch.int64, device="cuda")
+    check(lib.rfx_search_timed(ix.handle, ptr(q), 256, 10, None, 0, off, ptr(s), ptr(r), None, ptr(ws), ws.numel(),
+                               stream_ptr(None), None, None))
+    torch.cuda.synchronize()
+    assert ix.screen_diag(256, 10, ws)[1] == (mode == 2)
+    rec = rec.cpu().numpy()
+    assert np.array_equal(rec[..., 1], r.cpu().numpy())
+    assert np.array_equal((rec[..., 0] & 0xffffffff).astype(np.uint32).view(np.float32), s.cpu().numpy())
+    ix.enable_screen(1)
+
+
 def test_small_and_empty(rindex):
     ix = rindex.DeviceIndex(768, "bf16")
     ix.enable_screen(1)

@@ -87,3 +87,42 @@ def test_zero_query_keeps_every_row():
     y = np.zeros((1, 768), dtype=np.float32)
     s, r, nsv = oscreen.screen_topk(y, x, 5)
     assert nsv[0] == 100 and list(r[0]) == [0, 1, 2, 3, 4]
+
+
+def test_survivors_cover_the_f32_score_rule():
+    """Under the score rule every plan answers with (fl32 of the exact dot desc, row asc): a row whose
+    exact score is just below the k-th but rounds to the same f32 and has a smaller row id belongs in the
+    answer, so it must survive the cut A >= a_k - e2 (e2 carries two f32 ulps of the k-th score for it,
+    ADVICE r4).  Near-ties planted: copies of each query's k-th row with one element moved by one bf16
+    step, placed at smaller row ids (exact scores differ by ~1e-9, most round to the same f32)."""
+    from oracle import synth as osy
+    n, d, k = 4000, 768, 10
+    x = _corpus(n, d, "bf16")
+    y = _queries(6, d, "bf16")
+    ex = y.astype(np.float64) @ x.astype(np.float64).T
+    slot = 0
+    for i in range(y.shape[0]):
+        kth = int(np.lexsort((np.arange(n), -ex[i]))[k - 1])
+        for j in range(3):
+            v = x[kth].astype(np.float64).copy()
+            e = int(np.argsort(np.abs(y[i].astype(np.float64) * v))[j])  # the smallest score change
+            # one bf16 step of element e, in the direction that lowers the score a little
+            step = np.float64(np.ldexp(1.0, int(np.frexp(abs(v[e]) or 1e-3)[1]) - 8))
+            v[e] -= np.sign(y[i, e] or 1.0) * step
+            x[slot] = osy.bf16_bits_to_f32(osy.f32_to_bf16_bits(v.astype(np.float32)))
+            slot += 1
+    codes, scales, live, stats = oscreen.quantize_tiles(x)
+    qc, e2, _ = oscreen.quantize_queries(y, stats)
+    A = oscreen.screen_scores(codes, scales, qc)[:, :n]
+    ex = y.astype(np.float64) @ x.astype(np.float64).T
+    ties = 0
+    for i in range(y.shape[0]):
+        f32 = ex[i].astype(np.float32)
+        order = np.lexsort((np.arange(n), -f32))  # the score rule, on all rows
+        fk = f32[order[k - 1]]
+        want = np.nonzero(f32 >= fk)[0]  # every row the rule could place in the top k
+        ties += int(np.sum(f32 == fk)) - 1
+        ak = np.partition(A[i], n - k)[n - k]
+        t = np.float32(ak - e2[i])
+        assert (A[i, want] >= t).all()
+    assert ties >= 1  # the planted near-ties exist in f32

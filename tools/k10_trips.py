@@ -21,6 +21,7 @@ from rfx.index import DeviceIndex, synth_rows  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=1_250_000)
 ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--variant", type=int, default=80008192, help="a MODE-8192 variant (10**7 * RING + MODE)")
 a = ap.parse_args()
 f = _lib.lib.rfx_dbg_screen_variant
 f.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -35,11 +36,11 @@ ix.enable_screen(1)
 q = synth_rows(1, 0, 256, 768, "bf16")
 ws = torch.empty(ix.workspace_bytes(256, 10), dtype=torch.uint8, device="cuda")
 st = _lib.stream_ptr()
-_lib.check(f(ix.handle, _lib.ptr(q), 256, 10, 808192, _lib.ptr(ws), ws.numel(), st))  # warm
+_lib.check(f(ix.handle, _lib.ptr(q), 256, 10, a.variant, _lib.ptr(ws), ws.numel(), st))  # warm
 torch.cuda.synchronize()
 _lib.check(g(None, 1))
 for _ in range(a.reps):
-    _lib.check(f(ix.handle, _lib.ptr(q), 256, 10, 808192, _lib.ptr(ws), ws.numel(), st))
+    _lib.check(f(ix.handle, _lib.ptr(q), 256, 10, a.variant, _lib.ptr(ws), ws.numel(), st))
 torch.cuda.synchronize()
 t = np.zeros((2, 64), dtype=np.uint32)
 _lib.check(g(t.ctypes.data, 0))

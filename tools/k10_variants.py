@@ -2,7 +2,7 @@
 corpus in bursts of back-to-back launches, variants interleaved over rounds (the chip's clock
 settles per workload; cdna_hip_programming.md §5.4 rule 24).
 
-variant = 100000 * RING + MODE (k10_dbg.hip; round 3's logs used 1000 * RING + MODE): RING in {4, 6, 8, 10, 12}; MODE 1 = no top-k fold,
+variant = 10**7 * RING + MODE (k10_dbg.hip; round 4's logs used 100000 * RING + MODE, round 3's 1000 * RING + MODE): RING in {4, 6, 8, 10, 12}; MODE 1 = no top-k fold,
 8 = no corpus stream after the prologue, 9 = both; 32 = count slow-path entries (reported, not
 timed); 64 = the store-wide integer fast-path bound."""
 import argparse
@@ -26,7 +26,7 @@ ap.add_argument("--nq", type=int, default=256)
 ap.add_argument("--k", type=int, default=10)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--burst", type=int, default=30)
-ap.add_argument("--variants", default="800000,800001,800009,400000")
+ap.add_argument("--variants", default="80000000,80000001,80000009,40000000")
 ap.add_argument("--seconds", type=float, default=0.0, help="one variant back to back for this long (power sampling)")
 ap.add_argument("--validate", action="store_true", help="each variant's two-pass answer must equal production's")
 a = ap.parse_args()
@@ -62,7 +62,7 @@ if a.validate:  # every variant's two-pass answer (no fallback) against the prod
     vs.restype = ctypes.c_int
     ref_s, ref_r = ix.search(q, a.k)
     for v in variants:
-        if (v % 100000) & (1 | 8 | 512):  # timing-only variants (wrong results by design)
+        if (v % 10000000) & (1 | 8 | 512):  # timing-only variants (wrong results by design)
             continue
         s_ = torch.empty_like(ref_s)
         r_ = torch.empty_like(ref_r)
@@ -92,7 +92,7 @@ if a.seconds > 0:  # steady state of ONE variant (rocm-smi samples power / sclk 
 cnt = _lib.lib.rfx_dbg_screen_counts
 cnt.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
 cnt.restype = ctypes.c_int
-for v in [v for v in variants if (v % 100000) & 32]:  # slow-path entries of one launch (MODE 32 counter)
+for v in [v for v in variants if (v % 10000000) & 32]:  # slow-path entries of one launch (MODE 32 counter)
     launch(v)
     torch.cuda.synchronize()
     n = ctypes.c_uint64()
@@ -100,7 +100,7 @@ for v in [v for v in variants if (v % 100000) & 32]:  # slow-path entries of one
     ntiles = -(-a.rows // 32)
     print(json.dumps({"variant": v, "slow_path_wave_entries": n.value, "wave_tiles": ntiles * 8,
                       "frac": round(n.value / (ntiles * 8), 5)}))
-variants = [v for v in variants if not (v % 100000) & 32]
+variants = [v for v in variants if not (v % 10000000) & 32]
 res = {v: [] for v in variants}
 for rnd in range(a.rounds):
     for v in (variants if rnd % 2 == 0 else variants[::-1]):
