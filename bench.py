@@ -88,7 +88,8 @@ def parse():
     # (profiles/r04n/: 0.60 against 0.377 ms per shard step — the screen on the masked CUs and the select
     # on 8 CUs both lose more than the overlap hides)
     ap.add_argument("--pipeline", default="off", choices=["on", "off"])
-    ap.add_argument("--reserve-cus", type=int, default=8, help="--pipeline: CUs (bits 0..n-1 of the CU mask) for stream B")
+    ap.add_argument("--reserve-cus", type=int, default=8,
+                    help="--pipeline: CUs (bits 0..n-1 of the CU mask) for stream B; 0 = two unmasked streams")
     return ap.parse_args()
 
 
@@ -252,12 +253,18 @@ def main():
         for b in range(res):
             ma[b // 32] &= ~(1 << (b % 32)) & 0xffffffff
             mb[b // 32] |= 1 << (b % 32)
-        pa, pb = ctypes.c_void_p(), ctypes.c_void_p()
-        check(lib.rfx_stream_create_cu_mask(local, ma, nw, ctypes.byref(pa)))
-        check(lib.rfx_stream_create_cu_mask(local, mb, nw, ctypes.byref(pb)))
-        sA = torch.cuda.ExternalStream(pa.value, device=dev)
-        sB = torch.cuda.ExternalStream(pb.value, device=dev)
-        scan_blocks = ncu - res
+        if a.reserve_cus > 0:
+            pa, pb = ctypes.c_void_p(), ctypes.c_void_p()
+            check(lib.rfx_stream_create_cu_mask(local, ma, nw, ctypes.byref(pa)))
+            check(lib.rfx_stream_create_cu_mask(local, mb, nw, ctypes.byref(pb)))
+            sA = torch.cuda.ExternalStream(pa.value, device=dev)
+            sB = torch.cuda.ExternalStream(pb.value, device=dev)
+            scan_blocks = ncu - res
+        else:  # --reserve-cus 0: two plain streams over the whole chip; the hardware fills CUs that batch i's
+            # small kernels free with batch i+1's screen workgroups (no mask, the full 256-block screen)
+            res = 0
+            sA, sB = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+            scan_blocks = 0
         wsP = [ws, torch.empty_like(ws)]
         recP = [rec, torch.empty_like(rec)]
         gathP = [gathered, torch.empty_like(gathered)]

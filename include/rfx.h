@@ -210,6 +210,15 @@ int rfx_search_plan(rfx_index_t h, int64_t nq, int k, int* out_kernel);
  * {kept screen candidates, survivors re-scored (-1 = sent to the fallback)} into diag_h [nq][2], and
  * whether the exact fallback ran for the batch (*fallback_h != 0). */
 int rfx_screen_diag(rfx_index_t h, int64_t nq, int k, const void* ws_d, int32_t* diag_h, uint32_t* fallback_h);
+/* The score rule every rfx_search* answer follows (one rule for every plan, round 5): a score is fl32 of
+ * the f64 sum of the exact products of the stored row and query, the order (score desc, row asc).
+ * rfx_rescore_topk applies it in place to a [nq][k] answer assembled from the building blocks
+ * (rfx_scan_topk + rfx_topk_merge*, whose scores are the scan's own f32 sums): (scores_d, rows_d), or
+ * records_d [nq][k] {f32 score, i32 pad, i64 row} when not NULL; row_offset is subtracted from every row
+ * before it is read from this index (the base of a shard's records).  Rows < 0 (padding) stay last.
+ * Replaces no reference entry point: the reference's scores come from Gemini (gemini_rag.py:536). */
+int rfx_rescore_topk(rfx_index_t h, const void* queries_d, int64_t nq, int k, int64_t row_offset, float* scores_d,
+                     int64_t* rows_d, void* records_d, void* stream);
 /* rfx_search_masked writing [nq][k] merge records {f32 score, i32 pad, i64 row + row_offset} (the
  * all-gather input of the multi-GPU step) instead of scores and rows: one call per shard, whatever
  * kernel the plan picks (an empty shard writes padding records). */
@@ -263,6 +272,24 @@ int rfx_allgather_records(rfx_comm_t c, const void* const* sends_d, void* const*
  * caller's device when rank == root; group mode: local device index root), NULL elsewhere. */
 int rfx_gather_records(rfx_comm_t c, const void* const* sends_d, void* const* recvs_d, int root, int64_t nq,
                        int k, void* const* streams);
+
+/* One search over a store row-sharded across the GPUs of one process (the index-server topology,
+ * SURVEY §7; gemini_rag.py:721-725 get_rag_client -> one adapter over all the process's GPUs), issued from
+ * C++ so the host cost of a batch does not grow with Python calls per shard: every shard's whole search
+ * (rfx_search_records: kernel 10 / 11 where the shard holds its int8 copy) into [nq][k] records with
+ * bases[i] added, the exchange, one rfx_merge_gathered into (out_scores_d, out_rows_d) on streams[0].
+ *   handles / bases / streams / ws_d / ws_bytes / recs_d: per shard (n); queries_d on shard 0's device;
+ *   qbuf_d (may be NULL): per shard a [nq][dim] buffer on its device the queries are copied into first
+ *   (NULL entries, or the same pointer as queries_d: read in place — shards sharing shard 0's device);
+ *   masks_d / mask_words (may be NULL): per-shard row masks; gathered_d: [n][nq][k] records on shard 0's
+ *   device; comm: rfx_comm_init_all over the shards' devices in shard order (one RCCL gather to shard 0),
+ *   or 0 when every shard is on one device (logical shards; recs_d[i] may then BE row i of gathered_d);
+ *   src_stream: the stream that produced the queries, ordered before every shard and after the merge. */
+int rfx_sharded_search(int n, const rfx_index_t* handles, const int64_t* bases, const void* queries_d,
+                       void* const* qbuf_d, int64_t nq, int k, const uint32_t* const* masks_d,
+                       const int64_t* mask_words, void* const* ws_d, const size_t* ws_bytes, void* const* recs_d,
+                       void* gathered_d, rfx_comm_t comm, void* src_stream, void* const* streams,
+                       float* out_scores_d, int64_t* out_rows_d);
 
 /* ---- text → features (host) ---------------------------------------------------------------
  * The reference has no chunker/tokeniser of its own (chunking_config is forwarded to Gemini,

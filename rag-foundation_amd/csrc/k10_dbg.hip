@@ -5,7 +5,8 @@
 // 1024 serial LDS insert, 2048 slow-path issue priority, 4096 static tile split (no XCD balance),
 // 8192 slow-path entries and trips per tile index, 32768 no stage barriers, 65536 per-block start / end
 // wall clocks),
-// 131072 epilogue after the stage-0 barrier, 262144 waves 4-7 one stage later (stagger), 524288 partner
+// 131072 epilogue after the stage-0 barrier, 1048576 round 4's 64-bit list and float pass mask (round 5's
+// production fold: u32 scores + rows, integer pass threshold, per-position inserts in tiles 0-1), 262144 waves 4-7 one stage later (stagger), 524288 partner
 // bound by v_permlane16_swap (round 5),
 // via rfx_dbg_screen_variant; variant = 10^7 * RING + MODE (RING in {4, 6, 8, 10, 12}; rounds 3-4 used
 // 100000 * RING + MODE).
@@ -69,6 +70,9 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
     RFX_K10V(8, 655360)
     RFX_K10V(8, 917504)
     RFX_K10V(8, 131072 + 8192)
+    RFX_K10V(8, 1048576)
+    RFX_K10V(8, 1048576 + 8192)
+    RFX_K10V(8, 1048576 + 524288)
     RFX_K10V(8, 393216 + 8192)
     default:
       return -1;

@@ -260,6 +260,66 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
   }
 }
 
+// ---- round-5 fold (production; debug MODE kModeFold1 keeps round 4's 64-bit list) ------------------------
+// The lane's list as KL orderable scores S (best first, 0 = empty) beside their rows R.  An insert is
+// S'_i = max(S_i, min(S_{i-1}, key)) (the median of three for a sorted list) and, for the rows, with
+// c_i = (S_i >= key): R'_i = c_i ? R_i : (c_{i-1} ? row : R_{i-1}) — one compare, two selects and a
+// min/max pair per entry against round 4's 64-bit compare and four selects.  Equal scores keep their
+// order (the older, lower row ahead); which of two equal-score rows a full list keeps does not matter:
+// the select ranks survivors by their exact scores, and what falls out (min of the last entry and the
+// key) is the score `drop` records either way.  key 0 (an empty entry, below every real score) is a
+// no-op insert.
+template <int KL>
+__device__ __forceinline__ void insert_s(uint32_t (&S)[KL], uint32_t (&R)[KL], uint32_t key, uint32_t row,
+                                         uint32_t& drop_o) {
+  bool c[KL];
+#pragma unroll
+  for (int i = 0; i < KL; ++i) c[i] = S[i] >= key;
+  drop_o = max(drop_o, min(S[KL - 1], key));
+#pragma unroll
+  for (int i = KL - 1; i > 0; --i) {
+    R[i] = c[i] ? R[i] : (c[i - 1] ? row : R[i - 1]);
+    S[i] = max(S[i], min(S[i - 1], key));
+  }
+  R[0] = c[0] ? R[0] : row;
+  S[0] = max(S[0], key);
+}
+// The pass test of the slow path, (float)D * s_t >= tf, as ONE integer threshold per lane: t = min{D :
+// fl(fl(D) s_t) >= tf} (fl(D) exact: |D| < 2^24; the product's rounding is monotone in D, so the
+// passing D form an up-set).  From c = tf / s_t (v_rcp: |c - tf/s_t| < 1 for |c| <= 2^22) two steps
+// down while P(t - 1) and two up while !P(t) reach it exactly; `ok` verifies P(t) && !P(t - 1) (false
+// only for |c| > 2^22, where the wave takes the float mask instead).
+__device__ __forceinline__ int pass_threshold(float st, float tf, bool& ok) {
+  auto P = [&](int d) { return (float)d * st >= tf; };
+  if (!(tf > -__builtin_inff())) {
+    ok = true;
+    return INT_MIN;  // no bound yet: every value passes
+  }
+  if (!(st > 0.f)) {
+    ok = true;
+    return 0.f >= tf ? INT_MIN : INT_MAX;  // every A of the tile is 0
+  }
+  const float c = tf * __builtin_amdgcn_rcpf(st);
+  ok = fabsf(c) <= 4194304.f;
+  int t = ok ? (int)ceilf(c) : 0;
+  t -= P(t - 1) ? 1 : 0;
+  t -= P(t - 1) ? 1 : 0;
+  t += P(t) ? 0 : 1;
+  t += P(t) ? 0 : 1;
+  ok = ok && P(t) && !P(t - 1);
+  return t;
+}
+// The pass mask of the round-5 fold: bit r set = value r (acc[r >> 2][r & 3], row (r & 7) + 16 (r >> 3) of
+// the lane's half-tile) reaches the threshold; `all` before the live bits (pub: the lane publishes its
+// list's best), the return value after them.
+__device__ __forceinline__ uint32_t pass_mask_int(const v4i32 (&a)[4], int t, uint32_t bits, uint32_t& all) {
+  uint32_t pm = 0;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) pm |= a[r >> 2][r & 3] >= t ? (1u << r) : 0u;
+  all = pm;
+  return pm & ((bits & 0xffu) | ((bits >> 8) & 0xff00u));
+}
+
 // X: int8 codes [ntiles * 32][D]; tmeta: per tile {f32 scale, u32 live word, 0, 0}; stats: the
 // quantiser's maxima (stats[2] = max tile scale); Qc: int8 query codes [nq_pad][D];
 // qe2: [nq_pad] e2 per query (units of the query's scale).  Outputs per (query, list): KL
@@ -279,6 +339,7 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
 constexpr int kModeEpiLate = 131072;
 constexpr int kModeStagger = 262144;
 constexpr int kModePermBounds = 524288;
+constexpr int kModeFold1 = 1048576;  // round 4's 64-bit list + float mask (the round-5 fold is production)
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
@@ -355,9 +416,17 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   uint32_t* const ready = (uint32_t*)(lds + ctr_off<KL, RING>());  // MODE 32768: [RING] pieces landed
   uint32_t* const done = ready + 16;                                  // [RING] waves done reading
   if (tid < 32) ready[tid] = 0u;  // (the same zeros as the list init above)
-  uint64_t Lr[KL];  // production: the lane's list lives in registers for the whole scan
+  constexpr bool F2 = (MODE & kModeFold1) == 0 && (MODE & 1024) == 0;  // the round-5 fold
+  // (d 1024 holds 128 resident fragment registers: the unrolled per-position inserts would spill there)
+  constexpr bool SWEEP = D == 768;
+  uint64_t Lr[KL];  // round 4 (debug kModeFold1): the lane's 64-bit list in registers for the whole scan
+  uint32_t LS[KL], LR[KL];  // production: scores and rows (insert_s)
 #pragma unroll
-  for (int i = 0; i < KL; ++i) Lr[i] = 0ull;
+  for (int i = 0; i < KL; ++i) {
+    Lr[i] = 0ull;
+    LS[i] = 0u;
+    LR[i] = 0u;
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -551,8 +620,55 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
           }
         }
 #endif
-        fold_screen<KL, (MODE & 1024) == 0>(acc4, st, lw >> (8 * half), Ls, Lr, thr, e2, drop, tile * kTM + 8 * half,
-                                            tau_rsrc, slot_voff);
+        if constexpr (F2) {
+          const uint32_t bits = lw >> (8 * half);
+          const int rbase = tile * kTM + 8 * half;
+          const float tf = thr ? unord(thr) - e2 : -__builtin_inff();
+          bool ok;
+          const int tq = pass_threshold(st, tf, ok);
+          uint32_t all = 0, pm;
+          if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
+            pm = pass_mask_int(acc4, tq, bits, all);
+          } else {  // (|tf / s_t| > 2^22: the float test, exactly the round-4 mask)
+            bool pubf;
+            pm = fold_mask(acc4, st, bits, thr, e2, pubf);
+            all = pubf ? 1u : 0u;
+          }
+          if (SWEEP && it < 2) {
+            // the first tiles pass nearly every value (the list is empty, the bound not there yet): one
+            // insert per row position, the value taken from its register (no select tree); lanes without
+            // the position insert key 0 (a no-op)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const float sv = (float)acc4[r >> 2][r & 3] * st;
+              const uint32_t key = (pm >> r) & 1u ? ord(sv) : 0u;
+              insert_s<KL>(LS, LR, key, (uint32_t)(rbase + (r & 7) + 16 * (r >> 3)), drop);
+            }
+          } else {
+            while (pm) {
+              const int r = __builtin_ctz(pm);
+              pm &= pm - 1;
+              int m3 = -((r >> 3) & 1), m2 = -((r >> 2) & 1), m1 = -((r >> 1) & 1), m0 = -(r & 1);
+              asm volatile("" : "+v"(m3), "+v"(m2), "+v"(m1), "+v"(m0));
+              int v[8];
+#pragma unroll
+              for (int j = 0; j < 8; ++j) v[j] = (acc4[(j + 8) >> 2][j & 3] & m3) | (acc4[j >> 2][j & 3] & ~m3);
+#pragma unroll
+              for (int j = 0; j < 4; ++j) v[j] = (v[j + 4] & m2) | (v[j] & ~m2);
+#pragma unroll
+              for (int j = 0; j < 2; ++j) v[j] = (v[j + 2] & m1) | (v[j] & ~m1);
+              const int av = (v[1] & m0) | (v[0] & ~m0);
+              insert_s<KL>(LS, LR, ord((float)av * st), (uint32_t)(rbase + (r & 7) + 16 * (r >> 3)), drop);
+            }
+          }
+          if (all) {
+            thr = LS[KL - 1] > thr ? LS[KL - 1] : thr;
+            batomic_umax(tau_rsrc, slot_voff, LS[0]);
+          }
+        } else {
+          fold_screen<KL, (MODE & 1024) == 0>(acc4, st, lw >> (8 * half), Ls, Lr, thr, e2, drop, tile * kTM + 8 * half,
+                                              tau_rsrc, slot_voff);
+        }
         set_bounds();
         if constexpr ((MODE & 2048) != 0) __builtin_amdgcn_s_setprio(0);
       }
@@ -695,9 +811,9 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
     const int64_t o = ((int64_t)q * n_lists + lst) * KL;
 #pragma unroll
     for (int i = 0; i < KL; ++i) {
-      const uint64_t key = (MODE & 1024) == 0 ? Lr[i] : Ls[i * 64];
+      const uint64_t key = F2 ? (((uint64_t)LS[i] << 32) | (uint32_t)~LR[i]) : (MODE & 1024) == 0 ? Lr[i] : Ls[i * 64];
       const float sc = unord((uint32_t)(key >> 32));
-      const bool keep = key && sc >= lo;
+      const bool keep = (key >> 32) != 0 && sc >= lo;
       cand_s[o + i] = keep ? sc : -__builtin_inff();
       cand_r[o + i] = keep ? (int)(~(uint32_t)key) : kEmptyRow;
     }

@@ -180,6 +180,20 @@ __global__ __launch_bounds__(512) void merge_kernel(Src src, int list_len, int k
   if (rs.X) rescore_final(rs, (int64_t)blockIdx.x, k_out, row_offset, out_s, out_r, out_rec);
 }
 
+// The score rule applied to an answer in place (rfx_rescore_topk): one 256-thread block per query re-scores
+// its k entries (fl32 of the f64 dot with the index rows) and re-orders them (score desc, row asc).
+__global__ __launch_bounds__(256) void rescore_topk_kernel(Rescore rs, int k, int64_t row_offset, float* __restrict__ out_s,
+                                                           int64_t* __restrict__ out_r, MergeRec* __restrict__ out_rec) {
+  rescore_final(rs, (int64_t)blockIdx.x, k, row_offset, out_s, out_r, out_rec);
+}
+
+void launch_rescore_topk(const Rescore& rs, int64_t nq, int k, int64_t row_offset, float* out_s, int64_t* out_r,
+                         void* out_rec, hipStream_t st) {
+  if (nq <= 0) return;
+  hipLaunchKernelGGL(rescore_topk_kernel, dim3((unsigned)nq), dim3(256), 0, st, rs, k, row_offset, out_s, out_r,
+                     (MergeRec*)out_rec);
+}
+
 int launch_topk_merge_lists(const float* cs, const void* cr, int rows_are_i64, int64_t nq, int64_t n_cand,
                             int list_len, int k, int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec,
                             hipStream_t st, bool sorted, const uint32_t* gate, const Rescore* rescore) {

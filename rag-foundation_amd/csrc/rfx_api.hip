@@ -366,15 +366,19 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L, bool search
   L.fbk = 0;
   if (search && ix.screen && ix.rows > 0 && (L.kernel == 6 || L.kernel == 8)) {
     L.sp = rfx::plan_scan_screen(ix.rows, ix.dim, ix.dtype, nq, k, scan_blocks);
-    if (L.sp.ok) {
+    // the regions are sized (and placed) by the default plan, the most workgroups and lists any
+    // scan_blocks gives: every offset, the gate and diag words included, is then the same whatever
+    // scan_blocks a search used (rfx_screen_diag and rfx_search_plan build the default layout)
+    const rfx::MfmaPlan smax = scan_blocks ? rfx::plan_scan_screen(ix.rows, ix.dim, ix.dtype, nq, k, 0) : L.sp;
+    if (L.sp.ok && smax.ok) {
       L.fbk = L.kernel;
       L.kernel = 10;
-      const size_t nc = (size_t)L.sp.n_lists * L.sp.k_lane;
+      const size_t nc = (size_t)std::max(L.sp.n_lists, smax.n_lists) * std::max(L.sp.k_lane, smax.k_lane);
       L.s_tau = L.total;
-      L.s_cs = L.s_tau + align_up(rfx::tau_bytes_screen(L.sp));
+      L.s_cs = L.s_tau + align_up(std::max(rfx::tau_bytes_screen(L.sp), rfx::tau_bytes_screen(smax)));
       L.s_cr = L.s_cs + align_up((size_t)nq * nc * 4);
       L.s_drop = L.s_cr + align_up((size_t)nq * nc * 4);
-      L.s_qc = L.s_drop + align_up((size_t)nq * L.sp.n_lists * 4);
+      L.s_qc = L.s_drop + align_up((size_t)nq * std::max(L.sp.n_lists, smax.n_lists) * 4);
       L.s_qe2 = L.s_qc + align_up((size_t)L.sp.nq_pad * ix.dim);
       L.s_gate = L.s_qe2 + align_up((size_t)L.sp.nq_pad * 4);
       L.s_diag = L.s_gate + 256;
@@ -1071,6 +1075,23 @@ int rfx_topk_merge_lists(const float* cand_scores_d, const void* cand_rows_d, in
   return RFX_OK;
 }
 
+int rfx_rescore_topk(rfx_index_t h, const void* queries_d, int64_t nq, int k, int64_t row_offset, float* scores_d,
+                     int64_t* rows_d, void* records_d, void* stream) {
+  auto ix = get(h);
+  if (!ix) return fail(RFX_EINVAL, "unknown index handle");
+  if (k < 1 || k > 64) return fail(RFX_EINVAL, "k=%d out of range [1, 64]", k);
+  if (nq < 0) return fail(RFX_EINVAL, "nq < 0");
+  if (nq > 0 && (!queries_d || (!records_d && (!scores_d || !rows_d))))
+    return fail(RFX_EINVAL, "null queries / answer");
+  RFX_RLOCK(ix);
+  RFX_HIP(hipSetDevice(ix->device));
+  const rfx::Rescore rs{ix->data, queries_d, ix->dim, ix->dtype};
+  rfx::launch_rescore_topk(rs, nq, k, row_offset, records_d ? nullptr : scores_d, records_d ? nullptr : rows_d,
+                           records_d, (hipStream_t)stream);
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+
 int rfx_topk_merge_records(const float* cand_scores_d, const void* cand_rows_d, int rows_are_i64, int64_t nq,
                            int64_t n_cand, int list_len, int k, int64_t row_offset, void* out_records_d,
                            void* stream) {
@@ -1434,6 +1455,111 @@ int rfx_search_records(rfx_index_t h, const void* queries_d, int64_t nq, int k, 
   if (nq > 0 && !out_records_d) return fail(RFX_EINVAL, "null output");
   return search_impl(h, queries_d, nq, k, row_mask_d, mask_words, row_offset, nullptr, nullptr, out_records_d, ws_d,
                      ws_bytes, stream, nullptr, nullptr);
+}
+
+// ---- one search over a row-sharded store, issued from C++ -----------------------------------
+namespace {
+// events for the cross-stream orderings of rfx_sharded_search: per thread and device, reused call after
+// call (a stream that waited on an event keeps the state it saw when the wait was enqueued)
+hipEvent_t pooled_event(int device, int slot) {
+  thread_local std::map<int, std::vector<hipEvent_t>> pool;
+  auto& v = pool[device];
+  while ((int)v.size() <= slot) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    v.push_back(e);
+  }
+  return v[slot];
+}
+}  // namespace
+
+int rfx_sharded_search(int n, const rfx_index_t* handles, const int64_t* bases, const void* queries_d,
+                       void* const* qbuf_d, int64_t nq, int k, const uint32_t* const* masks_d,
+                       const int64_t* mask_words, void* const* ws_d, const size_t* ws_bytes, void* const* recs_d,
+                       void* gathered_d, rfx_comm_t comm, void* src_stream, void* const* streams,
+                       float* out_scores_d, int64_t* out_rows_d) {
+  if (n < 1 || !handles || !bases || !ws_d || !ws_bytes || !recs_d || !gathered_d || !streams)
+    return fail(RFX_EINVAL, "null shard arrays");
+  if (k < 1 || k > 64 || nq < 0) return fail(RFX_EINVAL, "k=%d / nq=%lld out of range", k, (long long)nq);
+  if (nq == 0) return RFX_OK;
+  if (!queries_d || !out_scores_d || !out_rows_d) return fail(RFX_EINVAL, "null queries / outputs");
+  std::vector<int> dev(n);
+  int64_t qbytes = 0;
+  for (int i = 0; i < n; ++i) {
+    auto ix = get(handles[i]);
+    if (!ix) return fail(RFX_EINVAL, "unknown index handle (shard %d)", i);
+    dev[i] = ix->device;
+    if (i == 0) qbytes = nq * ix->row_bytes();
+    if (!comm && dev[i] != dev[0]) return fail(RFX_EINVAL, "shards on several devices need a communicator");
+  }
+  const size_t rec_bytes = (size_t)nq * k * 16;
+  hipStream_t src = (hipStream_t)src_stream;
+  // 1. every shard stream after the queries (one event on the caller's stream)
+  int src_dev = dev[0];
+  RFX_HIP(hipSetDevice(src_dev));
+  hipEvent_t ev = pooled_event(src_dev, 0);
+  if (!ev) return fail(RFX_EDEVICE, "hipEventCreate failed");
+  RFX_HIP(hipEventRecord(ev, src));
+  for (int i = 0; i < n; ++i)
+    if ((hipStream_t)streams[i] != src) RFX_HIP(hipStreamWaitEvent((hipStream_t)streams[i], ev, 0));
+  // ... and after the previous search's merge on streams[0] (callers reuse the records and gathered buffers
+  // from search to search, and the previous merge may still be reading them)
+  if (n > 1) {
+    RFX_HIP(hipSetDevice(dev[0]));
+    hipEvent_t e0 = pooled_event(dev[0], n + 1);
+    if (!e0) return fail(RFX_EDEVICE, "hipEventCreate failed");
+    RFX_HIP(hipEventRecord(e0, (hipStream_t)streams[0]));
+    for (int i = 1; i < n; ++i)
+      if ((hipStream_t)streams[i] != (hipStream_t)streams[0]) RFX_HIP(hipStreamWaitEvent((hipStream_t)streams[i], e0, 0));
+  }
+  // 2. per shard: the queries on its device (a peer copy when it has a buffer there), then its whole search
+  // (rfx_search_records: the two-pass scan where the shard holds its int8 copy) into [nq][k] records with its
+  // base added
+  for (int i = 0; i < n; ++i) {
+    hipStream_t st = (hipStream_t)streams[i];
+    RFX_HIP(hipSetDevice(dev[i]));
+    const void* q = queries_d;
+    if (qbuf_d && qbuf_d[i] && qbuf_d[i] != queries_d) {
+      RFX_HIP(hipMemcpyAsync(qbuf_d[i], queries_d, (size_t)qbytes, hipMemcpyDeviceToDevice, st));
+      q = qbuf_d[i];
+    }
+    const int rc = search_impl(handles[i], q, nq, k, masks_d ? masks_d[i] : nullptr, mask_words ? mask_words[i] : 0,
+                               bases[i], nullptr, nullptr, recs_d[i], ws_d[i], ws_bytes[i], st, nullptr, nullptr);
+    if (rc) return rc;
+  }
+  // 3. the exchange: one RCCL gather to shard 0's device over distinct devices; shards sharing one device
+  // stack their records there (in place when recs_d[i] already is row i of gathered_d), ordered by events
+  if (comm) {
+    std::vector<void*> recvs((size_t)n, nullptr);
+    recvs[0] = gathered_d;
+    const int rc = rfx_gather_records(comm, (const void* const*)recs_d, recvs.data(), 0, nq, k, streams);
+    if (rc) return rc;
+  } else {
+    RFX_HIP(hipSetDevice(dev[0]));
+    for (int i = 0; i < n; ++i) {
+      hipStream_t st = (hipStream_t)streams[i];
+      uint8_t* dst = (uint8_t*)gathered_d + (size_t)i * rec_bytes;
+      if (recs_d[i] != dst) RFX_HIP(hipMemcpyAsync(dst, recs_d[i], rec_bytes, hipMemcpyDeviceToDevice, st));
+      if (i > 0 && st != (hipStream_t)streams[0]) {
+        hipEvent_t e = pooled_event(dev[0], i);
+        if (!e) return fail(RFX_EDEVICE, "hipEventCreate failed");
+        RFX_HIP(hipEventRecord(e, st));
+        RFX_HIP(hipStreamWaitEvent((hipStream_t)streams[0], e, 0));
+      }
+    }
+  }
+  // 4. the gathered merge on shard 0's stream; the caller's stream after it
+  RFX_HIP(hipSetDevice(dev[0]));
+  if (rfx::launch_merge_gathered(gathered_d, n, nq, k, out_scores_d, out_rows_d, (hipStream_t)streams[0]) != 0)
+    return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
+  RFX_HIP(hipGetLastError());
+  if ((hipStream_t)streams[0] != src) {
+    hipEvent_t e = pooled_event(dev[0], n);
+    if (!e) return fail(RFX_EDEVICE, "hipEventCreate failed");
+    RFX_HIP(hipEventRecord(e, (hipStream_t)streams[0]));
+    RFX_HIP(hipStreamWaitEvent(src, e, 0));
+  }
+  return RFX_OK;
 }
 
 int rfx_search_timed(rfx_index_t h, const void* queries_d, int64_t nq, int k, const uint32_t* row_mask_d,

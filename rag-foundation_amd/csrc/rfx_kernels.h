@@ -134,6 +134,8 @@ int launch_merge_gathered(const void* rec, int world, int64_t nq, int k, float* 
                           hipStream_t st);
 // n (score, row) pairs -> {score, 0, row + row_offset} merge records (rec) or (out_s, out_r + row_offset);
 // padding rows (< 0) stay -1
+void launch_rescore_topk(const Rescore& rs, int64_t nq, int k, int64_t row_offset, float* out_s, int64_t* out_r,
+                         void* out_rec, hipStream_t st);
 void launch_pack_records(const float* s, const int64_t* r, int64_t n, int64_t row_offset, void* rec, float* out_s,
                          int64_t* out_r, hipStream_t st);
 

@@ -145,6 +145,8 @@ SIGNATURES = {
     "rfx_search_masked": ([_u64, _p, _i64, _i, _p, _i64, _p, _p, _p, _sz, _p], _i),
     "rfx_search_records": ([_u64, _p, _i64, _i, _p, _i64, _i64, _p, _p, _sz, _p], _i),
     "rfx_search_plan": ([_u64, _i64, _i, _pi], _i),
+    "rfx_rescore_topk": ([_u64, _p, _i64, _i, _i64, _p, _p, _p, _p], _i),
+    "rfx_sharded_search": ([_i, _p, _p, _p, _p, _i64, _i, _p, _p, _p, _p, _p, _p, _u64, _p, _p, _p, _p], _i),
     "rfx_search_timed": ([_u64, _p, _i64, _i, _p, _i64, _i64, _p, _p, _p, _p, _sz, _p, _p, _p], _i),
     "rfx_search_staged": ([_u64, _p, _i64, _i, _p, _i64, _i64, _p, _p, _p, _p, _sz, _i, _i, _p], _i),
     "rfx_stream_create_cu_mask": ([_i, _p, _i, _pp], _i),

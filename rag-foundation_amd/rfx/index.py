@@ -338,6 +338,29 @@ def topk_merge_records(cand_s: torch.Tensor, cand_r: torch.Tensor, k: int, row_o
     return out
 
 
+def rescore_topk(index: "DeviceIndex", queries: torch.Tensor, scores: torch.Tensor = None, rows: torch.Tensor = None,
+                 records: torch.Tensor = None, row_offset: int = 0, stream=None):
+    """The score rule of every search (fl32 of the f64 dot; score desc, row asc) applied in place to an
+    answer assembled from scan_topk / topk_merge* (rfx_rescore_topk): (scores, rows) [nq][k], or the
+    [nq][k][2] records of topk_merge_records (rows carry row_offset).  Returns what it was given."""
+    q = index._check_queries(queries)
+    nq = q.shape[0]
+    if records is not None:
+        if records.shape[0] != nq or records.dim() != 3 or records.dtype != torch.int64 or not records.is_contiguous():
+            raise ValueError("records must be a contiguous int64 [nq][k][2] tensor")
+        k = records.shape[1]
+        with torch.cuda.device(q.device):
+            check(lib.rfx_rescore_topk(index.handle, ptr(q), nq, int(k), int(row_offset), None, None, ptr(records),
+                                       stream_ptr(stream)))
+        return records
+    if scores.shape != rows.shape or scores.shape[0] != nq or not (scores.is_contiguous() and rows.is_contiguous()):
+        raise ValueError("scores / rows must be contiguous [nq][k] tensors")
+    with torch.cuda.device(q.device):
+        check(lib.rfx_rescore_topk(index.handle, ptr(q), nq, int(scores.shape[1]), int(row_offset), ptr(scores),
+                                   ptr(rows), None, stream_ptr(stream)))
+    return scores, rows
+
+
 def merge_gathered(gathered: torch.Tensor, k: int, stream=None):
     """Final merge of all-gathered records [world][nq][k][2] int64 -> (scores [nq][k], rows [nq][k])."""
     if gathered.dim() != 4 or gathered.shape[3] != 2 or gathered.dtype != torch.int64 or gathered.shape[2] != k:

@@ -67,11 +67,12 @@ def _evict_union(key, closing):
 
 def _close_unions(closing):
     """Close evicted views outside _STATE_LOCK (hipFree may wait for the device), then uncount them."""
+    nbytes = sum(v.nbytes for v in closing)
     for v in closing:
         v.close()
     if closing:
         with _STATE_LOCK:
-            _UNION_BYTES[0] -= sum(v.nbytes for v in closing)
+            _UNION_BYTES[0] -= nbytes
 
 
 def _release_union(v):

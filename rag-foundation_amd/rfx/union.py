@@ -105,10 +105,9 @@ class UnionView:
             self.index.close()
             raise
         self._bases = np.asarray(self.bases, dtype=np.int64)
-
-    @property
-    def nbytes(self) -> int:
-        return self.index.rows * self.dim * (ESIZE[self.dtype] + (1 if self.screened else 0))
+        # device bytes (fixed: a follow writes into the regions' headroom, the rows never change); kept so
+        # the retriever's cache can uncount a view after closing it
+        self.nbytes = self.index.rows * self.dim * (ESIZE[self.dtype] + (1 if self.screened else 0))
 
     def _copy(self, st, r0, r1, append=False, base=0):
         span = 1 << 20

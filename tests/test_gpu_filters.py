@@ -112,9 +112,10 @@ def test_masked_scan_then_merge(rindex):
     allowed = np.random.default_rng(5).random(n) < 0.1
     ix, s, r = check_masked(rindex, n, dim, dtype, nq, k, allowed)
     m = torch.from_numpy(mask_words(allowed)).cuda()
-    cs, cr = ix.scan(rindex.synth_rows(12, 0, nq, dim, dtype), k, row_mask=m)
-    ms, mr = rindex.topk_merge(cs, cr, k)
-    assert np.array_equal(mr.cpu().numpy(), r)
+    q = rindex.synth_rows(12, 0, nq, dim, dtype)
+    cs, cr = ix.scan(q, k, row_mask=m)
+    ms, mr = rindex.rescore_topk(ix, q, *rindex.topk_merge(cs, cr, k))  # the search's score rule
+    assert np.array_equal(mr.cpu().numpy(), r) and np.array_equal(ms.cpu().numpy(), s)
 
 
 def test_mask_validation(rindex):

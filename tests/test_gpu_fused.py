@@ -1,7 +1,8 @@
 """GPU: the one-launch VALU search (rfx_search on a VALU plan: scan + last-block merge in one
 kernel, csrc/k_scan_valu.hip FUSED, per-stream zeroed launch state in rfx_api.hip).
 
-Bars: bit-identical to the three-launch path (rfx_scan_topk + rfx_topk_merge_lists) for every
+Bars: bit-identical to the three-launch path (rfx_scan_topk + rfx_topk_merge_lists, then the score rule
+rfx_rescore_topk) for every
 dtype / nq slice shape / k slot / row mask; repeated launches on one stream and launches on a second
 stream agree bit-for-bit (the launch state is returned to zero by every launch); config 2's
 shape (100k x 768 f32, nq 1, k 10) matches the CPU oracle (check_topk: rows exact outside the
@@ -24,8 +25,10 @@ def rindex():
 
 
 def three_launch(rindex, ix, q, k, row_mask=None):
+    # scan + merge, then the score rule every search answers with (rfx_rescore_topk: fl32 of the f64 dot,
+    # score desc, row asc); the one-launch search applies it in its last block
     cs, cr = ix.scan(q, k, row_mask=row_mask)
-    return rindex.topk_merge(cs, cr, k, list_len=ix.list_len(q.shape[0], k))
+    return rindex.rescore_topk(ix, q, *rindex.topk_merge(cs, cr, k, list_len=ix.list_len(q.shape[0], k)))
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16", "f16"])

@@ -152,7 +152,8 @@ def test_scan_then_records_then_gathered_equals_search(rindex):
         ix = rindex.DeviceIndex(d, "bf16")
         ix.add_synthetic(11, r1 - r0, gen_row0=r0)
         cs, cr = ix.scan(q, 10)
-        recs.append(rindex.topk_merge_records(cs, cr, 10, row_offset=r0, list_len=ix.list_len(256, 10)))
+        rec = rindex.topk_merge_records(cs, cr, 10, row_offset=r0, list_len=ix.list_len(256, 10))
+        recs.append(rindex.rescore_topk(ix, q, records=rec, row_offset=r0))  # the search's score rule
     s, r = rindex.merge_gathered(torch.stack(recs), 10)
     assert torch.equal(r, ref_r)
     assert torch.equal(s, ref_s)

@@ -298,3 +298,46 @@ def test_sharded_screened_store_equals_unsharded(tmp_path, monkeypatch):
     a_s, a_r = plain.registry.get(name).index.search(qs, 10)
     b_s, b_r = six.search(qs, 10)
     assert torch.equal(a_r, b_r) and torch.equal(a_s, b_s)
+
+
+@pytest.mark.parametrize("screen", [0, 1])
+def test_sharded_search_one_c_call_equals_python_path(tmp_path, screen):
+    """rfx_sharded_search (one C-ABI call: every shard's search, the exchange and the merge)
+    returns the per-shard Python path's answer bit for bit — masked and unmasked, for batches of several
+    sizes (its buffers are reused and grown), after growth that outgrows a shard's workspace, and against
+    the unsharded index."""
+    from rfx import filters
+    from rfx.index import DeviceIndex
+    from rfx.sharded import ShardedIndex
+
+    n = 200_003
+    whole = DeviceIndex(768, "bf16", 0)
+    whole.add_synthetic(21, n)
+    path = str(tmp_path / "rows.rfx")
+    whole.rows_append(path, 0)
+    sh = ShardedIndex(768, "bf16", [0, 0, 0, 0])
+    sh.rows_sync(path, n)
+    if screen:
+        whole.enable_screen(1)
+        sh.enable_screen(1)
+    words = filters.row_mask_words(n, [(5, 30_000), (90_000, 70_000), (199_000, 1003)])
+    m_whole = torch.from_numpy(words).cuda()
+    for nq in (256, 3, 100, 256, 1):
+        q = whole.read(7, nq * 5)[::5].contiguous()
+        for mask in (None, words):
+            sh.c_path = True
+            c = sh.search(q, 10, row_mask=sh.mask_tensor(words) if mask is not None else None)
+            sh.c_path = False
+            p = sh.search(q, 10, row_mask=sh.mask_tensor(words) if mask is not None else None)
+            w = whole.search(q, 10, row_mask=m_whole if mask is not None else None)
+            assert torch.equal(c[0], p[0]) and torch.equal(c[1], p[1]), (nq, mask is not None)
+            assert torch.equal(c[1], w[1]) and torch.equal(c[0], w[0]), (nq, mask is not None)
+    # the last shard grows (its workspace must grow with it: the call regrows and retries once)
+    whole.add_synthetic(21, 150_000, gen_row0=n)
+    whole.rows_append(path, n)
+    sh.rows_sync(path, n + 150_000)
+    q = whole.read(11, 256 * 3)[::3].contiguous()
+    sh.c_path = True
+    c = sh.search(q, 10)
+    w = whole.search(q, 10)
+    assert torch.equal(c[1], w[1]) and torch.equal(c[0], w[0])

@@ -1,0 +1,71 @@
+"""Dev tool: host issue cost of one search over a row-sharded store in ONE process (rfx.sharded.ShardedIndex,
+RFX_DEVICES=0x8 on a one-GPU box: 8 logical shards of config 3), against the GPU time of the same search
+(VERDICT r4 #5).  Both paths: the per-shard Python issue (RFX_SHARDED_C=0 semantics, ShardedIndex.c_path =
+False) and the one C-ABI call (rfx_sharded_search).
+
+host_issue_ms = wall time until search() returns, averaged over a burst enqueued back to back (the GPU is
+still busy: nothing here waits for it); gpu_ms = HIP events around the same burst / burst.
+Every answer of the C path is checked bit-for-bit against the Python path's."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "rag-foundation_amd"))
+import torch  # noqa: E402
+
+from rfx.index import synth_rows  # noqa: E402
+from rfx.sharded import ShardedIndex, parse_devices  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--rows", type=int, default=10_000_000)
+ap.add_argument("--devices", default="0x8")
+ap.add_argument("--nq", type=int, default=256)
+ap.add_argument("--k", type=int, default=10)
+ap.add_argument("--burst", type=int, default=20)
+ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--screen", type=int, default=1)
+a = ap.parse_args()
+
+devs = parse_devices(a.devices)
+sidx = ShardedIndex(768, "bf16", devs)
+cuts = sidx._cuts(a.rows)
+for i, sh in enumerate(sidx.shards):
+    sh.add_synthetic(0, cuts[i + 1] - cuts[i], gen_row0=cuts[i])
+    sidx.bases[i] = cuts[i]
+sidx._split = True
+if a.screen:
+    sidx.enable_screen(1)
+q = synth_rows(1, 0, a.nq, 768, "bf16", device=devs[0])
+torch.cuda.synchronize()
+
+res = {}
+answers = {}
+for rnd in range(a.rounds):
+    for c_path in (False, True):
+        sidx.c_path = c_path
+        for _ in range(3):
+            out = sidx.search(q, a.k)
+        torch.cuda.synchronize()
+        answers[c_path] = out
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        t0 = time.perf_counter()
+        for _ in range(a.burst):
+            sidx.search(q, a.k)
+        t_issue = (time.perf_counter() - t0) / a.burst
+        e1.record()
+        torch.cuda.synchronize()
+        gpu = e0.elapsed_time(e1) / a.burst
+        res.setdefault("c" if c_path else "python", []).append((t_issue * 1e3, gpu))
+same = torch.equal(answers[True][0], answers[False][0]) and torch.equal(answers[True][1], answers[False][1])
+out = {"rows": a.rows, "devices": a.devices, "nq": a.nq, "k": a.k, "burst": a.burst,
+       "plan": sidx.shards[0].search_plan(a.nq, a.k), "c_equals_python": bool(same)}
+for key, v in res.items():
+    out[key] = {"host_issue_ms": round(min(x[0] for x in v), 4), "gpu_ms_per_search": round(min(x[1] for x in v), 4),
+                "issue_over_gpu": round(min(x[0] for x in v) / min(x[1] for x in v), 3)}
+print(json.dumps(out, indent=1))
+if not same:
+    sys.exit("the C path's answer differs from the Python path's")
