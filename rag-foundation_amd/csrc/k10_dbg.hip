@@ -5,9 +5,9 @@
 // 1024 serial LDS insert, 2048 slow-path issue priority, 4096 static tile split (no XCD balance),
 // 8192 slow-path entries and trips per tile index, 32768 no stage barriers, 65536 per-block start / end
 // wall clocks),
-// 131072 epilogue after the stage-0 barrier, 1048576 round 4's 64-bit list and float pass mask (round 5's
-// production fold: u32 scores + rows, integer pass threshold, per-position inserts in tiles 0-1), 262144 waves 4-7 one stage later (stagger), 524288 partner
-// bound by v_permlane16_swap (round 5),
+// 131072 epilogue after the stage-0 barrier, 262144 waves 4-7 one stage later (stagger), 524288 partner
+// bound by v_permlane16_swap, 1048576 the round-5 u32-score fold (integer pass threshold, per-position
+// inserts in tiles 0-1; slower, not production), 2097152 one wait + barrier per tile (RING 10 / 12) (round 5),
 // via rfx_dbg_screen_variant; variant = 10^7 * RING + MODE (RING in {4, 6, 8, 10, 12}; rounds 3-4 used
 // 100000 * RING + MODE).
 #define RFX_K10_BLOCK_TIMES
@@ -29,51 +29,30 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
                        xcd_weights_device_ptr());                                                             \
     break;
   switch (variant) {
-    RFX_K10V(4, 0)
-    RFX_K10V(6, 0)
+    // (round 5 trimmed the list to the variants its tools run; earlier rounds' ring and MODE sweeps are in
+    // the profiles they wrote)
     RFX_K10V(8, 0)
-    RFX_K10V(10, 0)
-    RFX_K10V(12, 0)
     RFX_K10V(8, 1)
     RFX_K10V(8, 8)
     RFX_K10V(8, 9)
-    RFX_K10V(8, 2)
-    RFX_K10V(8, 4)
     RFX_K10V(8, 32)
-    RFX_K10V(4, 2)
-    RFX_K10V(4, 4)
-    RFX_K10V(8, 64)
-    RFX_K10V(8, 65)
-    RFX_K10V(8, 96)
-    RFX_K10V(8, 128)
-    RFX_K10V(8, 129)
-    RFX_K10V(8, 256)
-    RFX_K10V(8, 288)
     RFX_K10V(8, 512)
-    RFX_K10V(8, 1024)
-    RFX_K10V(8, 1056)
-    RFX_K10V(8, 16)
-    RFX_K10V(8, 48)
-    RFX_K10V(8, 2048)
-    RFX_K10V(8, 2080)
-    RFX_K10V(10, 32768)
-    RFX_K10V(10, 32800)
-    RFX_K10V(12, 32768)
-    RFX_K10V(8, 65536)
     RFX_K10V(8, 4096)
-    RFX_K10V(8, 4096 + 65536)
     RFX_K10V(8, 8192)
-    RFX_K10V(8, 131072)
-    RFX_K10V(8, 262144)
-    RFX_K10V(8, 393216)
+    RFX_K10V(8, 65536)
+    RFX_K10V(8, 4096 + 65536)
     RFX_K10V(8, 524288)
-    RFX_K10V(8, 655360)
-    RFX_K10V(8, 917504)
-    RFX_K10V(8, 131072 + 8192)
     RFX_K10V(8, 1048576)
     RFX_K10V(8, 1048576 + 8192)
-    RFX_K10V(8, 1048576 + 524288)
-    RFX_K10V(8, 393216 + 8192)
+    RFX_K10V(12, 0)
+    RFX_K10V(12, 2097152)
+    RFX_K10V(12, 2097152 + 8192)
+    RFX_K10V(12, 2097152 + 65536)
+    RFX_K10V(12, 2097152 + 524288)
+    RFX_K10V(12, 2097152 + 1048576)
+    RFX_K10V(10, 2097152)
+    RFX_K10V(12, 2097152 + 1)
+    RFX_K10V(12, 2097152 + 512)
     default:
       return -1;
   }

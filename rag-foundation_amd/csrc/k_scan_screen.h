@@ -260,7 +260,10 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
   }
 }
 
-// ---- round-5 fold (production; debug MODE kModeFold1 keeps round 4's 64-bit list) ------------------------
+// ---- round-5 fold (debug MODE kModeFold2; measured SLOWER than round 4's 64-bit list, which production keeps:
+// 0.407 against 0.340 ms at the 8-GPU shard, 2.327 against 2.104 ms at 10M rows, one box, interleaved,
+// profiles/r05/k10_fold2_ab_*.txt — the fewer VALU ops per insert did not pay for the larger code and
+// register footprint, 251 against 229 VGPRs) ------------------------------------------------------------
 // The lane's list as KL orderable scores S (best first, 0 = empty) beside their rows R.  An insert is
 // S'_i = max(S_i, min(S_{i-1}, key)) (the median of three for a sorted list) and, for the rows, with
 // c_i = (S_i >= key): R'_i = c_i ? R_i : (c_{i-1} ? row : R_{i-1}) — one compare, two selects and a
@@ -339,7 +342,8 @@ __device__ __forceinline__ uint32_t pass_mask_int(const v4i32 (&a)[4], int t, ui
 constexpr int kModeEpiLate = 131072;
 constexpr int kModeStagger = 262144;
 constexpr int kModePermBounds = 524288;
-constexpr int kModeFold1 = 1048576;  // round 4's 64-bit list + float mask (the round-5 fold is production)
+constexpr int kModeFold2 = 1048576;  // the round-5 u32-score fold (debug; slower, see above)
+constexpr int kModeTileBarrier = 2097152;  // one wait + barrier per tile (TB below; RING 12)
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
@@ -416,11 +420,11 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   uint32_t* const ready = (uint32_t*)(lds + ctr_off<KL, RING>());  // MODE 32768: [RING] pieces landed
   uint32_t* const done = ready + 16;                                  // [RING] waves done reading
   if (tid < 32) ready[tid] = 0u;  // (the same zeros as the list init above)
-  constexpr bool F2 = (MODE & kModeFold1) == 0 && (MODE & 1024) == 0;  // the round-5 fold
+  constexpr bool F2 = (MODE & kModeFold2) != 0 && (MODE & 1024) == 0;  // the round-5 fold (debug)
   // (d 1024 holds 128 resident fragment registers: the unrolled per-position inserts would spill there)
   constexpr bool SWEEP = D == 768;
-  uint64_t Lr[KL];  // round 4 (debug kModeFold1): the lane's 64-bit list in registers for the whole scan
-  uint32_t LS[KL], LR[KL];  // production: scores and rows (insert_s)
+  uint64_t Lr[KL];  // production: the lane's 64-bit list in registers for the whole scan
+  uint32_t LS[KL], LR[KL];  // debug kModeFold2: scores and rows (insert_s)
 #pragma unroll
   for (int i = 0; i < KL; ++i) {
     Lr[i] = 0ull;
@@ -540,7 +544,16 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   // stages behind the others without stalling them.  Pieces go out AHEAD = RING - 1 - LAG stages early.
   constexpr bool DEC = (MODE & 32768) != 0 && (MODE & 8) == 0;
   constexpr int LAG = DEC ? 3 : 0;
-  constexpr int AHEAD = RING - 1 - LAG;
+  // Debug kModeTileBarrier (TB): one wait + barrier per TILE (at its last stage) instead of one per stage.
+  // Stage h's piece goes out at k-step 0 of stage h - AHEAD, AHEAD = RING - NST, into the slot of stage
+  // h - RING, which the barrier of the tile before has freed; the tile-t barrier waits for every stage of
+  // tile t + 1.  A wave in the slow path then has the rest of the tile's k-steps, not one stage's, before
+  // the next rendezvous.  The slot table refreshed after tile t's barrier is read at tile t + TBD's start
+  // (TBD: the first tile whose barrier wait covers that refresh without waiting for younger pieces).
+  constexpr bool TB = (MODE & kModeTileBarrier) != 0 && !DEC && (MODE & 8) == 0;
+  constexpr int AHEAD = TB ? RING - NST : RING - 1 - LAG;
+  static_assert(!TB || RING >= 2 * NST + 2, "TB: at least two stages beyond the next tile in flight");
+  constexpr int TBD = TB ? ((RING - NST + NST - 1) / NST > 2 ? (RING - NST + NST - 1) / NST : 2) : 2;
   constexpr int RA = AHEAD + 1;           // the counted-wait arithmetic below is in stages in flight
   static_assert(AHEAD >= 3, "at least three stages in flight");
   constexpr int YNG = (RA - 2) * kGPW;  // ops younger than the next stage
@@ -551,10 +564,16 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   issue_tau();
 #pragma unroll
   for (int p = 0; p < AHEAD; ++p) issue_piece(p, p);
-  // stage 0 landed: younger are stages 1 .. AHEAD - 1 and the metadata records issued with stages
-  // 0 .. AHEAD - 1 (with piece 0's own record after it)
-  constexpr int NM0 = (AHEAD - 1) / NST + 1;
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(YNG + NM0) : "memory");
+  if constexpr (TB) {
+    // tile 0 landed: younger are the pieces of stages NST .. AHEAD - 1 and their tile records
+    constexpr int NMT = (AHEAD - 1) / NST;  // records of stages NST, 2 NST, ... <= AHEAD - 1
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((AHEAD - NST) * kGPW + NMT) : "memory");
+  } else {
+    // stage 0 landed: younger are stages 1 .. AHEAD - 1 and the metadata records issued with stages
+    // 0 .. AHEAD - 1 (with piece 0's own record after it)
+    constexpr int NM0 = (AHEAD - 1) / NST + 1;
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(YNG + NM0) : "memory");
+  }
   if constexpr (DEC)
     if (lane == 0) lds_arrive(&ready[0]);  // stage 0's first use of slot 0 counts like every other
   asm volatile("s_barrier" ::: "memory");
@@ -678,7 +697,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   };
   auto tile_body = [&](const int it, v4i32(&acc4)[4], v4i32(&accp)[4], const bool prev) {
     const int gbase = it * NST;
-    if (it >= 2 && tau_refresh_tile<MODE>(it - 2)) {
+    if (it >= TBD && tau_refresh_tile<MODE>(it - TBD)) {
       thr = max(thr, (MODE & 256) != 0 ? tau_min<KL>(tq) : tau_kth<KL>(tq));
       set_bounds();
     }
@@ -710,7 +729,31 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
               if (h >= RING) lds_spin_ge(&done[h % RING], (uint32_t)(8 * (h / RING)));
             issue_piece(h, h % RING);
           }
-        if (kk == KB) {
+        if (kk == KB && TB) {
+          if (s == NST - 1) {
+            // tile it + 1 landed: younger are the pieces of stages NST (it + 2) .. NST (it + 1) + RING - 1, their
+            // tile records, and the refreshes issued after the last needed piece that tile it + 1 does not read
+            // (tiles it + 2 - TBD .. it - 1); the refresh tile it + 1 reads (tile it + 1 - TBD) comes right
+            // after that piece and is waited for
+            constexpr int NMY = (RING - NST - 1) / NST;
+            int nt_ = 0;
+#pragma unroll
+            for (int d = 1; d <= TBD - 2; ++d) nt_ += (it >= d && tau_refresh_tile<MODE>(it - d)) ? kTauGPW : 0;
+            static_assert(kTauGPW == 2, "wait table below");
+            switch (nt_) {
+#define RFX_K10_TWAIT(N)                                                                                      \
+  case N:                                                                                                     \
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"((RING - 2 * NST) * kGPW + NMY + N) : "memory");        \
+    break;
+              RFX_K10_TWAIT(0) RFX_K10_TWAIT(2)
+              default:  // stricter, never looser
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"((RING - 2 * NST) * kGPW + NMY) : "memory");
+#undef RFX_K10_TWAIT
+            }
+            asm volatile("s_barrier" ::: "memory");
+            if (tau_refresh_tile<MODE>(it)) issue_tau();
+          }
+        } else if (kk == KB) {
           if constexpr ((MODE & 8) == 0) {
             // younger than stage g+1's piece: stages g+2 .. g+RA-1 (YNG), the metadata records issued
             // with stages g+1 .. g+RA-1 that start a tile (nmeta(s): s = g mod NST), a refresh
