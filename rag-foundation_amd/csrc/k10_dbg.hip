@@ -51,6 +51,9 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
     RFX_K10V(12, 2097152 + 524288)
     RFX_K10V(12, 2097152 + 1048576)
     RFX_K10V(10, 2097152)
+    RFX_K10V(10, 2097152 + 8192)
+    RFX_K10V(10, 2097152 + 512)
+    RFX_K10V(10, 2097152 + 1)
     RFX_K10V(12, 2097152 + 1)
     RFX_K10V(12, 2097152 + 512)
     default:

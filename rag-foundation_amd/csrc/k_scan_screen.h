@@ -262,7 +262,7 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
 
 // ---- round-5 fold (debug MODE kModeFold2; measured SLOWER than round 4's 64-bit list, which production keeps:
 // 0.407 against 0.340 ms at the 8-GPU shard, 2.327 against 2.104 ms at 10M rows, one box, interleaved,
-// profiles/r05/k10_fold2_ab_*.txt — the fewer VALU ops per insert did not pay for the larger code and
+// profiles/r05/k10_fold2_tb_ab_*.txt — the fewer VALU ops per insert did not pay for the larger code and
 // register footprint, 251 against 229 VGPRs) ------------------------------------------------------------
 // The lane's list as KL orderable scores S (best first, 0 = empty) beside their rows R.  An insert is
 // S'_i = max(S_i, min(S_{i-1}, key)) (the median of three for a sorted list) and, for the rows, with
@@ -880,22 +880,28 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
 #endif
 }
 
+// Production schedule (round 5): one counted wait + barrier per TILE (kModeTileBarrier) over a 10-slot ring —
+// against round 4's wait + barrier per stage over 8 slots: 2.004 against 2.054 ms at 10M rows, 0.3313 against
+// 0.3393 ms at the 8-GPU shard (one box, interleaved, profiles/r05/k10_tb_ab_*.txt); round 4's schedule stays
+// in the debug library as variant (8, 0).
+constexpr int kProdRing = 10;
+constexpr int kProdMode = kModeTileBarrier;
 // one translation unit per D instantiates the kernel for KL in {4, 10}, with and without a filter mask
 #define RFX_K10_INSTANTIATE(DV, NAME)                                                                         \
   int NAME(int kl, dim3 grid, hipStream_t st, const int8_t* X, const uint4* tm, const uint32_t* sts,           \
            const int8_t* Qc, const float* qe2, int nq, int ntiles, uint32_t* tau, float* cs, int* cr,          \
            uint32_t* dr, int64_t n_lists, const uint32_t* mask, uint32_t* xb, uint32_t* xw) {               \
     if (kl == 4 && !mask)                                                                                   \
-      hipLaunchKernelGGL((scan_screen_kernel<4, DV, false>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,   \
+      hipLaunchKernelGGL((scan_screen_kernel<4, DV, false, kProdRing, kProdMode>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,   \
                          ntiles, tau, cs, cr, dr, n_lists, mask, xb, xw);                                    \
     else if (kl == 10 && !mask)                                                                             \
-      hipLaunchKernelGGL((scan_screen_kernel<10, DV, false>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,  \
+      hipLaunchKernelGGL((scan_screen_kernel<10, DV, false, kProdRing, kProdMode>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,  \
                          ntiles, tau, cs, cr, dr, n_lists, mask, xb, xw);                                    \
     else if (kl == 4)                                                                                       \
-      hipLaunchKernelGGL((scan_screen_kernel<4, DV, true>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,    \
+      hipLaunchKernelGGL((scan_screen_kernel<4, DV, true, kProdRing, kProdMode>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,    \
                          ntiles, tau, cs, cr, dr, n_lists, mask, xb, xw);                                    \
     else if (kl == 10)                                                                                      \
-      hipLaunchKernelGGL((scan_screen_kernel<10, DV, true>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,   \
+      hipLaunchKernelGGL((scan_screen_kernel<10, DV, true, kProdRing, kProdMode>), grid, dim3(512), 0, st, X, tm, sts, Qc, qe2, nq,   \
                          ntiles, tau, cs, cr, dr, n_lists, mask, xb, xw);                                    \
     else                                                                                                    \
       return -1;                                                                                            \

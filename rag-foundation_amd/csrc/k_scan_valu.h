@@ -190,15 +190,18 @@ __device__ __forceinline__ void merge_one(const Src& src, int64_t q, int list_le
                                           float* __restrict__ out_s, int64_t* __restrict__ out_r,
                                           MergeRec* __restrict__ out_rec);
 
+// The scan's body, a device function over VIRTUAL blocks: vblk (< nvb) stands for blockIdx.x (its rows,
+// its candidate list) and the FUSED arrival counts nvb virtual blocks, so the final merge runs once
+// every virtual block has finished, whichever workgroups ran them.  The kernel below runs one virtual
+// block per workgroup (vblk = blockIdx.x); kernel 11 (k_screen_valu.hip) runs its exact fallback inside
+// its own launch by having its workgroups CLAIM virtual blocks from a counter (round 5): the fallback
+// completes whichever of them run, so it needs no co-residency of the grid.
 template <int DT, int NQT, int K, int VPL, bool FUSED>
-__global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restrict__ X, int nrows, int D,
-                                                        const void* __restrict__ Qf, int nq,
-                                                        int rows_per_wave, float* __restrict__ cand_s,
-                                                        int* __restrict__ cand_r, int n_lists,
-                                                        const uint32_t* __restrict__ mask,
-                                                        uint32_t* __restrict__ tau, FusedOut fo) {
-  if constexpr (FUSED)  // gated (the two-pass scan's fallback): the whole grid returns together
-    if (fo.gate && __hip_atomic_load(fo.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+__device__ __forceinline__ void scan_valu_body(const uint8_t* __restrict__ X, int nrows, int D,
+                                               const void* __restrict__ Qf, int nq, int rows_per_wave,
+                                               float* __restrict__ cand_s, int* __restrict__ cand_r,
+                                               int n_lists, const uint32_t* __restrict__ mask,
+                                               uint32_t* __restrict__ tau, const FusedOut& fo, int vblk, int nvb) {
   constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
   constexpr int EPV = 16 / ESZ;
   extern __shared__ __attribute__((aligned(16))) float q_lds[];  // [NQT][D]
@@ -208,7 +211,7 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
   const int nqt = min(NQT, nq - q0);
   const int VPR = D * ESZ / 16;
   const int64_t RB = (int64_t)D * ESZ;
-  const int wave_g = blockIdx.x * 4 + (tid >> 6);
+  const int wave_g = vblk * 4 + (tid >> 6);
   const int wb = (int)min((int64_t)wave_g * rows_per_wave, (int64_t)nrows);
   const int we = (int)min((int64_t)wb + rows_per_wave, (int64_t)nrows);
 
@@ -369,7 +372,7 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
       bound = max(seen[(qi - w) / 4], mine);
     }
     if (lane < K) {
-      const int64_t o = ((int64_t)(q0 + qi) * n_lists + blockIdx.x) * K + lane;
+      const int64_t o = ((int64_t)(q0 + qi) * n_lists + vblk) * K + lane;
       const bool keep = M.lr != kEmptyRow && ord_f32(M.ls) >= bound;
       const float cs_v = keep ? M.ls : -__builtin_inff();
       const int cr_v = keep ? M.lr : kEmptyRow;
@@ -394,10 +397,12 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
     if (tid == 0) {
       const uint32_t old =
           __hip_atomic_fetch_add(fo.ctr + blockIdx.y, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = old == gridDim.x - 1;
+      last = old == (uint32_t)nvb - 1u;
     }
     __syncthreads();
-    if (!last) return;
+    // (readfirstlane: a uniform branch for the compiler, so a caller's loop around this body keeps its
+    // barriers in uniform control flow; kernel 11's claim loop below hung without it, round 5)
+    if (!__builtin_amdgcn_readfirstlane(last)) return;
     const int64_t n = (int64_t)n_lists * K;
     if (n <= kFusedLdsCand) {
       // Bulk copy first: every candidate of the query is loaded with all loads in flight (one
@@ -444,6 +449,19 @@ __global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restric
     if (tid < nqt && tau) tau[q0 + tid] = 0u;  // every block's bound updates precede its arrival
     if (tid == 0) fo.ctr[blockIdx.y] = 0u;
   }
+}
+
+template <int DT, int NQT, int K, int VPL, bool FUSED>
+__global__ __launch_bounds__(256) void scan_valu_kernel(const uint8_t* __restrict__ X, int nrows, int D,
+                                                        const void* __restrict__ Qf, int nq,
+                                                        int rows_per_wave, float* __restrict__ cand_s,
+                                                        int* __restrict__ cand_r, int n_lists,
+                                                        const uint32_t* __restrict__ mask,
+                                                        uint32_t* __restrict__ tau, FusedOut fo) {
+  if constexpr (FUSED)  // gated (the two-pass scan's fallback): the whole grid returns together
+    if (fo.gate && __hip_atomic_load(fo.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
+  scan_valu_body<DT, NQT, K, VPL, FUSED>(X, nrows, D, Qf, nq, rows_per_wave, cand_s, cand_r, n_lists, mask, tau, fo,
+                                         (int)blockIdx.x, (int)gridDim.x);
 }
 
 // K values instantiated for the scan; runtime k is rounded up to one of these and only the

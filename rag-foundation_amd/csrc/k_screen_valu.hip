@@ -1,8 +1,9 @@
 // k_screen_valu.hip — kernel 11: the exact two-pass scan for a lone question or a handful (nq <= 8;
 // BASELINE config 2: 100k × 768 f32, nq 1, k 10, and the adapter's un-batched questions), in ONE
 // launch: int8 screen of the index's int8 copy on v_dot4_i32_i8, exact re-score of the rows that can
-// still reach the top-k, the final merge in the last block.  A gated launch of the exact one-launch
-// VALU search (k_scan_valu.h) follows and runs only when the screen cannot prove its answer.
+// still reach the top-k, the final merge in the last block.  When the screen cannot prove its answer
+// the exact one-launch VALU search (k_scan_valu.h) rewrites it: for a lone question inside this same
+// launch (round 5, below), otherwise as a gated launch that follows.
 //
 // Path: the retrieval half of GeminiRag.ask_stream (backend/app/services/gemini_rag.py:517-551).
 // The int8 copy and the exactness argument are kernel 10's (k_scan_screen.h): per
@@ -13,11 +14,17 @@
 //     its 15 best (A, row) and, in entry 15, its drop bound (everything it did not keep is <= it);
 //   * the last block to finish (agent-scope arrival counter) takes a_k' = the k-th best A over the
 //     records' best entries (a lower bound of a_k: distinct live rows).  If some drop bound
-//     reaches a_k' - e2 a dropped row might belong to the top-k: it sets the gate and the exact
-//     one-launch search that follows rewrites the answer.  Otherwise every row with
+//     reaches a_k' - e2 a dropped row might belong to the top-k: not proven, and the exact search
+//     rewrites the answer.  Otherwise every row with
 //     A >= a_k' - e2 (the top-k among them, as a_k' <= a_k) is in a record: it re-scores those survivors exactly (f64 sum of the
 //     exact products, rounded to f32, 16 lanes per row) and ranks them (score desc, row asc).
 // No atomics on shared addresses besides the arrival counter: the bound travels in the records.
+// The fallback inside the launch (lone question): the blocks that arrived before the last one wait, for
+// a bounded time, for its verdict; on "not proven" every block still there, and the last block itself,
+// CLAIMS virtual blocks of the exact search from a counter (scan_valu_body over vb) until none is left.
+// A block that stops waiting simply exits, so the fallback is complete whichever blocks take part —
+// no co-residency of the grid is needed (round 4 withdrew a version that split the search statically
+// over the waiting blocks: two launches on one device could fill every CU with waiting blocks).
 // Algorithmic bytes: N·d codes + ⌈N/32⌉·16 tile records + the re-scored rows (a few per query).
 #include "k_scan_valu.h"
 
@@ -79,6 +86,31 @@ __device__ unsigned long long g_k11_last[8];
   } while (0)
 #endif
 
+// The exact fallback inside kernel 11's launch (a lone question): claim virtual blocks of the one-launch
+// VALU search (K slot 16) until all are taken.  Every branch around a barrier here is on a readfirstlane
+// value (uniform to the compiler): with the claimed unit read as a plain LDS value the compiler structurised
+// the loop as a divergent one — lanes 1-63 of wave 0 went back to the barrier before lane 0 claimed the
+// next unit, and the block re-ran one unit forever (round 5, a 120-s test timeout).  Bounded: a block
+// claims at most gridDim.x units.
+template <int DT, int D, int VPLV>
+__device__ __attribute__((noinline)) void k11_fallback(const void* X, int nrows, const void* Q, int nq, int rows_per_wave,
+                                                       float* cand_s, int* cand_r, const uint32_t* mask, uint32_t* vtau,
+                                                       uint32_t* vctr, uint32_t* clm, int k_out, float* out_s,
+                                                       int64_t* out_r) {
+  __shared__ int unit;
+  const int tid = threadIdx.x;
+  for (int it = 0; it <= (int)gridDim.x; ++it) {
+    if (tid == 0) unit = (int)__hip_atomic_fetch_add(clm, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const int u = __builtin_amdgcn_readfirstlane(unit);
+    __syncthreads();
+    if (u >= (int)gridDim.x) break;
+    scan_valu_body<DT, 1, 16, VPLV, true>((const uint8_t*)X, nrows, D, Q, nq, rows_per_wave, cand_s, cand_r,
+                                          (int)gridDim.x, mask, vtau, FusedOut{vctr, k_out, out_s, out_r, nullptr}, u,
+                                          (int)gridDim.x);
+  }
+}
+
 template <int DT, int D, int NQT>
 __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restrict__ X8, const uint4* __restrict__ tmeta,
                                                           const uint32_t* __restrict__ stats, int nrows,
@@ -86,7 +118,8 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
                                                           int rows_per_wave, const uint32_t* __restrict__ mask,
                                                           uint32_t* __restrict__ state, float* __restrict__ cand_s,
                                                           int* __restrict__ cand_r, int k_out, float* __restrict__ out_s,
-                                                          int64_t* __restrict__ out_r, int force) {
+                                                          int64_t* __restrict__ out_r, int force,
+                                                          uint32_t* __restrict__ vtau, uint32_t* __restrict__ vctr) {
   constexpr int C = D / 256;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, j = lane & 15;
   const int n_lists = gridDim.x;
@@ -94,7 +127,29 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   // fallback gate (written by the last block, read by the gated exact search)
   uint32_t* const ctr = state;
   uint32_t* const gate = state + 24;
+  // The in-launch fallback's words, each on a cache line of its own (the waiting blocks poll the
+  // verdict; polling the arrival counter's line slowed every block's arrival, round 4): [32] the launch
+  // generation g (read by every block at its start, advanced by the last block once all have arrived),
+  // [64] the verdict 4 g + 1 (proven) / 4 g + 2 (not proven), [96] the claim counter (reset by the last
+  // block before a "not proven" verdict).  A verdict names its launch, so nothing is reset after it;
+  // launches sharing this state are ordered on one stream, so no block of launch g runs beside g + 1.
+  uint32_t* const genw = state + 32;
+  uint32_t* const dec = state + 64;
+  uint32_t* const clm = state + 96;
+  constexpr int ESZV = DT == RFX_F32 ? 4 : 2;
+  constexpr int VPR0 = D * ESZV / 16;
+  constexpr int VPLV = (VPR0 + 15) / 16 <= 4 ? 4 : (VPR0 + 15) / 16 <= 8 ? 8 : (VPR0 + 15) / 16 <= 12 ? 12 : 16;
+  constexpr bool INL = screen_valu_inline_fallback(NQT, DT, D);
+  // the exact fallback: claim virtual blocks of the one-launch VALU search (K slot 16) until all are taken
+  // (a call, not inlined: the fallback's registers stay out of the screen's allocation — inlined, kernel 11
+  // went from 256 to 256 + 57 AGPR registers and its screen from 41.6 to 49.8 us at config 2, round 5)
+  auto fallback = [&]() {
+    if constexpr (INL)
+      k11_fallback<DT, D, VPLV>(X, nrows, Q, nq, rows_per_wave, cand_s, cand_r, mask, vtau, vctr, clm, k_out, out_s,
+                                out_r);
+  };
   RFX_K11_T(0);
+  const uint32_t gen0 = INL ? __hip_atomic_load(genw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
 
   // The int8 row stream (step 2): iteration t scores rows wb + 64 (t >> 4) + 4 (t & 15) + g.  Its first
   // NB - 1 iterations of loads are issued here, before the query quantiser, so their latency overlaps
@@ -335,12 +390,36 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   }
   __syncthreads();
   RFX_K11_T(3);
-  if (!last) return;
+  const bool lastu = __builtin_amdgcn_readfirstlane(last) != 0;  // (uniform: see fallback above)
+  if (!INL && !lastu) return;
+  if (!lastu) {
+    // wait for the last block's verdict on this launch, at most kVerdictWait of wall clock (100 MHz):
+    // a block that stops waiting exits, and the fallback completes without it
+    constexpr uint64_t kVerdictWait = 10000;  // 100 us
+    __shared__ uint32_t verdict;
+    if (tid == 0) {
+      const uint64_t t0 = wall_clock64();
+      uint32_t d = 0u;
+      for (;;) {
+        d = __hip_atomic_load(dec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (((d >> 2) == (gen0 & 0x3fffffffu) && (d & 3u)) || wall_clock64() - t0 > kVerdictWait) break;
+        __builtin_amdgcn_s_sleep(8);
+      }
+      verdict = (d >> 2) == (gen0 & 0x3fffffffu) ? (d & 3u) : 0u;
+    }
+    __syncthreads();
+    if (__builtin_amdgcn_readfirstlane(verdict) == 2u) fallback();
+    return;
+  }
   RFX_K11_L(0);
   if (force & 8) {
     if (tid == 0) {
       *gate = 0u;
       *ctr = 0u;
+      if (INL) {
+        __hip_atomic_store(dec, ((gen0 & 0x3fffffffu) << 2) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(genw, gen0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     return;
   }
@@ -529,9 +608,22 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     if (qi == 0) RFX_K11_L(4);
   }
   RFX_K11_L(5);
+  const bool fb = __builtin_amdgcn_readfirstlane(fail) != 0;
   if (tid == 0) {
-    *gate = fail ? 1u : 0u;  // read by the gated exact search that follows on the stream
+    // the gate: read by the gated exact search that follows on the stream (several questions)
+    __hip_atomic_store(gate, fb ? 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *ctr = 0u;
+    if (INL) {
+      // the claim counter is zero before any block can read a "not proven" verdict
+      if (fb) __hip_atomic_store(clm, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(dec, ((gen0 & 0x3fffffffu) << 2) | (fb ? 2u : 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(genw, gen0 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (INL && fb) {
+    __syncthreads();
+    fallback();
   }
 }
 
@@ -544,16 +636,23 @@ int dbg_k11_times(unsigned long long* blocks_h, unsigned long long* last_h) {
 }
 #endif
 
-// One launch: grid (blocks) × 256 threads, one query slice of up to 8 queries.
+// One launch: grid (blocks) × 256 threads, one query slice of up to 8 queries.  The in-launch fallback
+// (a lone question) is the one-launch VALU search's K slot 16 over the same plan (k 5..16; its state
+// vstate: bounds, then counters).
 int launch_screen_valu(const ValuPlan& p, const int8_t* X8, const void* tmeta, const uint32_t* stats, int nrows, int D,
                        int dtype, const void* X, const void* Q, int nq, const uint32_t* mask, uint32_t* state,
-                       float* cs, int* cr, int k, float* out_s, int64_t* out_r, int force, hipStream_t st) {
+                       uint32_t* vstate, float* cs, int* cr, int k, float* out_s, int64_t* out_r, int force,
+                       hipStream_t st) {
   if (nq < 1 || nq > 8 || k < 1 || k > kK || (D != 768 && D != 1024)) return -1;
   if ((int64_t)p.blocks * kK > (int64_t)1 << 30) return -1;
+  if (screen_valu_inline_fallback(nq == 1 ? 1 : 8, dtype, D) && (!vstate || p.q_slices != 1 || valu_k_slot(k) != 16))
+    return -1;
   const dim3 grid((unsigned)p.blocks);
+  uint32_t* const vtau = vstate;
+  uint32_t* const vctr = vstate ? vstate + kValuFusedMaxNq : nullptr;
 #define RFX_SV(DTV, DV, NQ)                                                                                      \
   hipLaunchKernelGGL((screen_valu_kernel<DTV, DV, NQ>), grid, dim3(256), 0, st, X8, (const uint4*)tmeta, stats, nrows, \
-                     X, Q, nq, p.rows_per_wave, mask, state, cs, cr, k, out_s, out_r, force)
+                     X, Q, nq, p.rows_per_wave, mask, state, cs, cr, k, out_s, out_r, force, vtau, vctr)
 #define RFX_SV_D(DTV)                  \
   if (D == 768) {                      \
     if (nq == 1)                       \

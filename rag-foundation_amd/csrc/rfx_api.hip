@@ -557,6 +557,28 @@ int k11_ablate() {
 
 // Kernel 11 (k_screen_valu.hip): a few questions (nq <= 8) on an index holding the int8 copy, on a
 // VALU plan with lists of 16 (5 <= k <= 16) — one launch, plus the gated exact one-launch search.
+// Kernel-11 launches of one device run one at a time, whatever stream they are issued on: each waits
+// for the device's previous one (an event) when that one went to another stream.  Kernel 11 holds one
+// workgroup per CU and its early blocks wait (bounded) for the last one's verdict; two such launches
+// side by side would fill the CUs with waiting blocks until the bound ends the waits (correct — the
+// in-launch fallback needs no co-residency — but slow).
+struct K11Order {
+  std::mutex mu;
+  hipEvent_t ev = nullptr;
+  hipStream_t last = nullptr;
+  bool used = false;
+};
+K11Order& k11_order(int device) {
+  static K11Order o[64];
+  return o[device & 63];
+}
+// RFX_K11_UNORDERED=1 (tests, read at every search): no ordering — the in-launch fallback's
+// correctness without it
+bool k11_unordered() {
+  const char* e = getenv("RFX_K11_UNORDERED");
+  return e && e[0] == '1';
+}
+
 bool screen_valu_eligible(const Index& ix, const SearchLayout& L, int64_t nq, int k) {
   return ix.screen && ix.rows > 0 && L.kernel == 0 && nq >= 1 && nq <= 8 && k <= 16 && L.vp.k_slot == 16 &&
          rfx::screen_supported(ix.dim, ix.dtype) && fused_enabled();
@@ -1384,19 +1406,31 @@ int search_impl(rfx_index_t h, const void* queries_d, int64_t nq, int k, const u
   };
   if ((!pack || L.pk_off) && screen_valu_eligible(*ix, L, nq, k) && ((uintptr_t)queries_d & 15) == 0) {
     uint32_t* state = nullptr;
-    std::unique_lock<std::mutex> slk(ix->state_mu);  // held until both launches are enqueued
+    std::unique_lock<std::mutex> slk(ix->state_mu);  // held until the launches are enqueued
     if ((rc = fused_state(*ix, st, &state, slk))) return rc;
     uint32_t* sv = state + rfx::kScreenValuState;
+    K11Order& ko = k11_order(ix->device);
+    std::lock_guard<std::mutex> olk(ko.mu);
+    if (!ko.ev) RFX_HIP(hipEventCreateWithFlags(&ko.ev, hipEventDisableTiming));
+    if (ko.used && ko.last != st && !k11_unordered()) RFX_HIP(hipStreamWaitEvent(st, ko.ev, 0));
     if ((rc = mark(ev0))) return rc;
+    // one launch for a lone question: the screen, and the exact one-launch search run by the same
+    // launch when the screen cannot prove its answer (its state: the front of the same search state)
     if (rfx::launch_screen_valu(L.vp, ix->scodes, ix->smeta, ix->sstats, (int)ix->rows, ix->dim, ix->dtype, ix->data,
-                                queries_d, (int)nq, row_mask_d, sv, cs, cr, k, vo_s, vo_r,
+                                queries_d, (int)nq, row_mask_d, sv, state, cs, cr, k, vo_s, vo_r,
                                 (ix->screen == 2 ? 1 : 0) | k11_ablate(), st) != 0)
       return fail(RFX_EUNSUPPORTED, "two-pass VALU search launch rejected");
+    RFX_HIP(hipEventRecord(ko.ev, st));
+    ko.last = st;
+    ko.used = true;
     if ((rc = mark(ev1))) return rc;
-    // the exact one-launch search, gated on the word the screen's last block wrote
-    if (rfx::launch_search_valu_fused(L.vp, ix->data, (int)ix->rows, ix->dim, ix->dtype, queries_d, (int)nq, cs, cr,
-                                      state, k, vo_s, vo_r, st, row_mask_d, sv + 24) != 0)
-      return fail(RFX_EUNSUPPORTED, "VALU search launch rejected");
+    if (!rfx::screen_valu_inline_fallback(nq == 1 ? 1 : 8, ix->dtype, ix->dim)) {
+      // several questions (or f32 rows at d 1024): the exact one-launch search, gated on the word the
+      // screen's last block wrote
+      if (rfx::launch_search_valu_fused(L.vp, ix->data, (int)ix->rows, ix->dim, ix->dtype, queries_d, (int)nq, cs, cr,
+                                        state, k, vo_s, vo_r, st, row_mask_d, sv + 24) != 0)
+        return fail(RFX_EUNSUPPORTED, "VALU search launch rejected");
+    }
     RFX_HIP(hipGetLastError());
     slk.unlock();
     return finish_pack();

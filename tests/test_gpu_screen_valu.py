@@ -131,3 +131,71 @@ def test_kernel11_small_stores(rindex):
         s, r = _check(ix, rows32, q, q32, 10)
         if n < 10:
             assert (r[0, n:] == -1).all()
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+def test_kernel11_lone_question_fallback_in_launch(rindex, dtype):
+    """A lone question runs the exact fallback INSIDE kernel 11's launch (round 5: workgroups claim
+    virtual blocks of the one-launch VALU search): forced (screen mode 2) and natural (40 copies of the
+    winner, more than a wave list holds), each equal to the exact scan; the state a fallback leaves does
+    not leak into the next screened search."""
+    ix, rows32 = _make(rindex, 60000, 768, dtype, screen=0)
+    q, q32 = _queries(rindex, 3, 768, dtype)
+    exact = [_check(ix, rows32, q[i:i + 1].contiguous(), q32[i:i + 1], 10) for i in range(3)]
+    for mode in (2, 1, 2, 1):
+        ix.enable_screen(mode)
+        assert ix.search_plan(1, 10) == 11
+        for i in range(3):
+            s, r = _check(ix, rows32, q[i:i + 1].contiguous(), q32[i:i + 1], 10)
+            assert np.array_equal(r, exact[i][1]) and np.array_equal(s, exact[i][0])
+    top = int(osearch.topk(q32[:1].astype(np.float64), rows32.astype(np.float64), 1)[1][0, 0])
+    ix.enable_screen(0)
+    first = ix.add(ix.read(top, 1).repeat(40, 1))
+    rows32 = np.concatenate([rows32, np.repeat(rows32[top:top + 1], 40, axis=0)])
+    ix.enable_screen(1)
+    s, r = _check(ix, rows32, q[:1].contiguous(), q32[:1], 16)
+    assert r[0, 0] == top and list(r[0, 1:16]) == list(range(first, first + 15))
+
+
+@pytest.mark.parametrize("unordered", [False, True])
+def test_kernel11_from_two_streams_at_once(rindex, monkeypatch, unordered):
+    """Kernel 11 issued from two streams of one device at once: a store sharded over four logical shards
+    of this GPU (each shard's search on its own stream) plus a second store on a third stream, lone
+    questions, the screen forced to decline half the time (the in-launch fallback runs while other
+    kernel-11 launches are in flight).  librfx orders kernel-11 launches per device; with that ordering
+    switched off (RFX_K11_UNORDERED=1) launches overlap and waiting blocks may give up, and the answers
+    must still be the oracle's."""
+    from rfx.sharded import ShardedIndex
+    if unordered:
+        monkeypatch.setenv("RFX_K11_UNORDERED", "1")
+    n = 120_000
+    sh = ShardedIndex(768, "f32", [0, 0, 0, 0])
+    cuts = sh._cuts(n)
+    for i, s in enumerate(sh.shards):
+        s.add_synthetic(51, cuts[i + 1] - cuts[i], gen_row0=cuts[i])
+        sh.bases[i] = cuts[i]
+    sh._split = True
+    rows_a = _widen(osynth.synth_rows(51, 0, n, 768, "f32"), "f32")
+    ix_b, rows_b = _make(rindex, 50_000, 768, "bf16", seed=52)
+    q, q32 = _queries(rindex, 12, 768, "f32", seed=53)
+    qb, qb32 = _queries(rindex, 12, 768, "bf16", seed=54)
+    side = torch.cuda.Stream()
+    outs = []
+    for rnd, mode in enumerate((1, 2, 1, 2)):
+        sh.enable_screen(mode)
+        ix_b.enable_screen(mode)
+        for i in range(12):
+            a = sh.search(q[i:i + 1].contiguous(), 10)
+            with torch.cuda.stream(side):
+                b = ix_b.search(qb[i:i + 1].contiguous(), 10, stream=side)
+            outs.append((rnd, i, a, b))
+        assert all(s.search_plan(1, 10) == 11 for s in sh.shards) and ix_b.search_plan(1, 10) == 11
+    torch.cuda.synchronize()
+    ra64, rb64 = rows_a.astype(np.float64), rows_b.astype(np.float64)
+    for rnd, i, a, b in outs:
+        for (s, r), rows64, qq in ((a, ra64, q32[i:i + 1]), (b, rb64, qb32[i:i + 1])):
+            s, r = s.cpu().numpy(), r.cpu().numpy()
+            q64 = qq.astype(np.float64)
+            ref_s, ref_r = osearch.topk(q64, rows64, 10)
+            probs = osearch.check_topk(s, r, ref_s, ref_r, lambda qi, rr: rows64[rr] @ q64[qi], tol=TOL, tie_band=TIE)
+            assert not probs, (rnd, i, probs[:5])
