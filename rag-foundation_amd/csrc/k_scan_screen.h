@@ -175,6 +175,48 @@ __device__ __forceinline__ uint32_t fold_mask(const v4i32 (&a)[4], float st, uin
   }
   return pm;
 }
+// Production pass mask (round 5): one INTEGER threshold per lane instead of 16 float scale-and-compare
+// steps.  t is at or below the smallest D with fl(fl(D) s_t) >= thr - e2 (the passing D form an up-set:
+// the product's rounding is monotone in D), so the mask is a superset of the float test's: a value it adds
+// lies below thr - e2 <= a_k - e2, is looked at like any other (kept, or recorded in drop) and can never
+// reach the select's a_k - e2 (the records hold the true top-k, so the select's a_k' is a_k).  The margin:
+// c = tf * rcp(s_t) is within 2^-22 |c| of tf / s_t, and fl(D s_t) >= tf needs D >= tf / s_t (1 - 2^-24);
+// |c| 2^-19 + 2 covers both.  The 16 bits are shifted in by v_alignbit (the sign of t - 1 - D, which
+// is set iff D >= t; |D| < 2^24, |t| <= 2^30: no overflow): 2 VALU per value against the float test's 4.
+// (debug kModeFloatMask: the float test, fold_mask above)
+__device__ __forceinline__ uint32_t fold_mask_int(const v4i32 (&a)[4], float st, uint32_t bits, uint32_t thr_o, float e2,
+                                                  bool& pub) {
+  int mx = max3i(a[0][0], a[0][1], a[0][2]);
+  mx = max3i(mx, a[0][3], a[1][0]);
+  mx = max3i(mx, a[1][1], a[1][2]);
+  mx = max3i(mx, a[1][3], a[2][0]);
+  mx = max3i(mx, a[2][1], a[2][2]);
+  mx = max3i(mx, a[2][3], a[3][0]);
+  mx = max3i(mx, a[3][1], a[3][2]);
+  mx = max(mx, a[3][3]);
+  const float tf = thr_o ? unord(thr_o) - e2 : -__builtin_inff();
+  constexpr int kBig = 1 << 30;
+  int t;
+  if (!(tf > -__builtin_inff())) {
+    t = -kBig;  // no bound yet: every value
+  } else if (!(st > 0.f)) {
+    t = 0.f >= tf ? -kBig : kBig;  // every A of the tile is 0
+  } else {
+    const float c = tf * __builtin_amdgcn_rcpf(st);
+    const float cl = floorf(c - fabsf(c) * 0x1p-19f) - 2.f;
+    t = (int)fminf(fmaxf(cl, -1073741824.f), 1073741824.f);
+  }
+  pub = mx >= t;
+  uint32_t pm = 0;
+  if (pub) {
+    const int tm1 = t - 1;
+#pragma unroll
+    for (int r = 15; r >= 0; --r)  // MSB first: value r ends at bit r
+      pm = __builtin_amdgcn_alignbit(pm, (uint32_t)(tm1 - a[r >> 2][r & 3]), 31);
+    pm &= (bits & 0xffu) | ((bits >> 8) & 0xff00u);
+  }
+  return pm;
+}
 // One passing value of this lane (the lowest bit of pm, cleared) into its list.
 template <int KL>
 __device__ __forceinline__ void fold_trip(const v4i32 (&a)[4], float st, int rbase, uint32_t& pm, uint64_t (&L)[KL],
@@ -220,13 +262,13 @@ __device__ __forceinline__ void fold_end(const uint64_t (&L)[KL], uint32_t& thr_
     batomic_umax(tau_rsrc, slot_voff, (uint32_t)(L[0] >> 32));
   }
 }
-template <int KL, bool REG = true>
+template <int KL, bool REG = true, bool FMASK = false>
 __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint32_t bits, uint64_t* Ls, uint64_t (&L)[KL],
                                             uint32_t& thr_o,
                                             float e2, uint32_t& drop_o, int rbase, v4i32 tau_rsrc, uint32_t slot_voff) {
   if constexpr (REG) {
     bool pub;
-    uint32_t pm = fold_mask(a, st, bits, thr_o, e2, pub);
+    uint32_t pm = FMASK ? fold_mask(a, st, bits, thr_o, e2, pub) : fold_mask_int(a, st, bits, thr_o, e2, pub);
     // one passing value per lane per trip: the wave makes max-over-lanes(popcount) trips, not one
     // trip per position some lane passes at
     while (pm) fold_trip<KL>(a, st, rbase, pm, L, drop_o);
@@ -344,6 +386,7 @@ constexpr int kModeStagger = 262144;
 constexpr int kModePermBounds = 524288;
 constexpr int kModeFold2 = 1048576;  // the round-5 u32-score fold (debug; slower, see above)
 constexpr int kModeTileBarrier = 2097152;  // one wait + barrier per tile (TB below; RING 12)
+constexpr int kModeFloatMask = 4194304;  // the slow path's float pass mask (fold_mask) instead of fold_mask_int
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
@@ -629,7 +672,8 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
 #ifdef RFX_K10_BLOCK_TIMES
         if constexpr ((MODE & 8192) != 0) {
           bool pub_;
-          const uint32_t pm_ = fold_mask(acc4, st, lw >> (8 * half), thr, e2, pub_);
+          const uint32_t pm_ = (MODE & kModeFloatMask) != 0 ? fold_mask(acc4, st, lw >> (8 * half), thr, e2, pub_)
+                                                             : fold_mask_int(acc4, st, lw >> (8 * half), thr, e2, pub_);
           int c = __popc(pm_);
 #pragma unroll
           for (int off = 32; off; off >>= 1) c = max(c, __shfl_xor(c, off));
@@ -685,7 +729,8 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
             batomic_umax(tau_rsrc, slot_voff, LS[0]);
           }
         } else {
-          fold_screen<KL, (MODE & 1024) == 0>(acc4, st, lw >> (8 * half), Ls, Lr, thr, e2, drop, tile * kTM + 8 * half,
+          fold_screen<KL, (MODE & 1024) == 0, (MODE & kModeFloatMask) != 0>(acc4, st, lw >> (8 * half), Ls, Lr, thr, e2, drop,
+                                                                              tile * kTM + 8 * half,
                                               tau_rsrc, slot_voff);
         }
         set_bounds();

@@ -395,7 +395,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   if (!lastu) {
     // wait for the last block's verdict on this launch, at most kVerdictWait of wall clock (100 MHz):
     // a block that stops waiting exits, and the fallback completes without it
-    constexpr uint64_t kVerdictWait = 10000;  // 100 us
+    constexpr uint64_t kVerdictWait = 5000;  // 50 us
     __shared__ uint32_t verdict;
     if (tid == 0) {
       const uint64_t t0 = wall_clock64();

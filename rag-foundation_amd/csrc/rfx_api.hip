@@ -185,7 +185,10 @@ int fused_state(Index& ix, hipStream_t st, uint32_t** out, const std::unique_loc
   uint32_t* p = nullptr;
   const size_t bytes = (size_t)rfx::kValuFusedStateWords * 4;
   if (hipMalloc(&p, bytes) != hipSuccess) return fail(RFX_ENOMEM, "hipMalloc(%zu) failed (search state)", bytes);
-  RFX_HIP(hipMemset(p, 0, bytes));  // synchronous: zero before the first launch on any stream
+  // zeroed on the stream that will use it: hipMemset is asynchronous to the host and runs on the null
+  // stream, which a non-blocking stream does not wait for (round 5: a first search on a fresh torch
+  // stream could read the state before it was zeroed)
+  RFX_HIP(hipMemsetAsync(p, 0, bytes, st));
   ix.fused_state[st] = p;
   *out = p;
   return RFX_OK;
@@ -557,16 +560,19 @@ int k11_ablate() {
 
 // Kernel 11 (k_screen_valu.hip): a few questions (nq <= 8) on an index holding the int8 copy, on a
 // VALU plan with lists of 16 (5 <= k <= 16) — one launch, plus the gated exact one-launch search.
-// Kernel-11 launches of one device run one at a time, whatever stream they are issued on: each waits
-// for the device's previous one (an event) when that one went to another stream.  Kernel 11 holds one
-// workgroup per CU and its early blocks wait (bounded) for the last one's verdict; two such launches
-// side by side would fill the CUs with waiting blocks until the bound ends the waits (correct — the
-// in-launch fallback needs no co-residency — but slow).
+// Kernel-11 launches of one device run one at a time once more than one stream issues them: each then
+// waits for the device's previous one (an event) when that one went to another stream.  Kernel 11 holds
+// one workgroup per CU and its early blocks wait (bounded) for the last one's verdict; two such launches
+// side by side can fill the CUs with waiting blocks until the bound ends the waits (correct — the
+// in-launch fallback needs no co-residency — but slow).  A device whose kernel-11 launches all come from
+// one stream records nothing (an event record per search cost config 2 ~5 us a search, round 5).
 struct K11Order {
   std::mutex mu;
   hipEvent_t ev = nullptr;
   hipStream_t last = nullptr;
   bool used = false;
+  bool multi = false;     // a second stream has issued kernel 11 on this device
+  bool recorded = false;  // ev holds the previous launch
 };
 K11Order& k11_order(int device) {
   static K11Order o[64];
@@ -1412,7 +1418,10 @@ int search_impl(rfx_index_t h, const void* queries_d, int64_t nq, int k, const u
     K11Order& ko = k11_order(ix->device);
     std::lock_guard<std::mutex> olk(ko.mu);
     if (!ko.ev) RFX_HIP(hipEventCreateWithFlags(&ko.ev, hipEventDisableTiming));
-    if (ko.used && ko.last != st && !k11_unordered()) RFX_HIP(hipStreamWaitEvent(st, ko.ev, 0));
+    if (ko.used && ko.last != st) {
+      ko.multi = true;
+      if (ko.recorded && !k11_unordered()) RFX_HIP(hipStreamWaitEvent(st, ko.ev, 0));
+    }
     if ((rc = mark(ev0))) return rc;
     // one launch for a lone question: the screen, and the exact one-launch search run by the same
     // launch when the screen cannot prove its answer (its state: the front of the same search state)
@@ -1420,7 +1429,10 @@ int search_impl(rfx_index_t h, const void* queries_d, int64_t nq, int k, const u
                                 queries_d, (int)nq, row_mask_d, sv, state, cs, cr, k, vo_s, vo_r,
                                 (ix->screen == 2 ? 1 : 0) | k11_ablate(), st) != 0)
       return fail(RFX_EUNSUPPORTED, "two-pass VALU search launch rejected");
-    RFX_HIP(hipEventRecord(ko.ev, st));
+    if (ko.multi) {
+      RFX_HIP(hipEventRecord(ko.ev, st));
+      ko.recorded = true;
+    }
     ko.last = st;
     ko.used = true;
     if ((rc = mark(ev1))) return rc;
