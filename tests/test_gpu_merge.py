@@ -212,5 +212,8 @@ def test_sorted_merge_of_every_scan_plan(rindex, dtype, nq):
             a_s, a_r = rindex.topk_merge(cs, cr, k, list_len=ll)
             b_s, b_r = rindex.topk_merge(cs, cr, k, list_len=ll, sorted=True)
             assert torch.equal(a_r, b_r) and torch.equal(a_s, b_s), (ix.plan(nq, k), m is None, k)
+            # the search applies the one score rule (fl32 of the f64 dot, score desc / row asc) to its final
+            # k; the merged scan candidates carry the scan's f32 sums until rescore_topk applies it
             c_s, c_r = ix.search(q, k, row_mask=m)
-            assert torch.equal(c_r, a_r) and torch.equal(c_s, a_s)
+            e_s, e_r = rindex.rescore_topk(ix, q, a_s.clone(), a_r.clone())
+            assert torch.equal(c_r, e_r) and torch.equal(c_s, e_s), (ix.plan(nq, k), m is None, k)
