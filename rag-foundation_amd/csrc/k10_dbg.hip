@@ -8,7 +8,8 @@
 // 131072 epilogue after the stage-0 barrier, 262144 waves 4-7 one stage later (stagger), 524288 partner
 // bound by v_permlane16_swap, 1048576 the round-5 u32-score fold (integer pass threshold, per-position
 // inserts in tiles 0-1; slower, not production), 2097152 one wait + barrier per tile (RING 10 / 12; production
-// at RING 10), 4194304 the slow path's float pass mask instead of the integer threshold (round 5),
+// at RING 10), 4194304 the slow path's float pass mask instead of the integer threshold, 16384 a sorted
+// merge instead of the pop loop when some lane passes >= 8 values (round 5),
 // via rfx_dbg_screen_variant; variant = 10^7 * RING + MODE (RING in {4, 6, 8, 10, 12}; rounds 3-4 used
 // 100000 * RING + MODE).
 #define RFX_K10_BLOCK_TIMES
@@ -57,6 +58,8 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
     RFX_K10V(10, 2097152 + 1)
     RFX_K10V(10, 2097152 + 4194304)
     RFX_K10V(10, 2097152 + 4194304 + 8192)
+    RFX_K10V(10, 2097152 + 16384)
+    RFX_K10V(10, 2097152 + 16384 + 8192)
     RFX_K10V(12, 2097152 + 1)
     RFX_K10V(12, 2097152 + 512)
     default:

@@ -262,16 +262,86 @@ __device__ __forceinline__ void fold_end(const uint64_t (&L)[KL], uint32_t& thr_
     batomic_umax(tau_rsrc, slot_voff, (uint32_t)(L[0] >> 32));
   }
 }
-template <int KL, bool REG = true, bool FMASK = false>
+// Debug kModeSortMerge (round 5): a wave whose lanes pass many values at once (the first tiles, where
+// every value passes: 16 pop-loop trips each) folds them as one sorted merge instead of one trip per
+// value: the lane's 16 keys (orderable A << 32 | ~row, 0 = not passing) are sorted by a bitonic network,
+// and the top KL of the union with the list come out of a bitonic split (max(L[i], K[KL-1-i]): the
+// top KL of the union, as a bitonic sequence) re-sorted; the best key not kept is
+// max(min(L[i], K[KL-1-i]), K[KL]) — what the trips would have recorded in drop, and the same list.
+__device__ __forceinline__ void cx_desc64(uint64_t& a, uint64_t& b) {
+  const bool sw = a < b;
+  const uint64_t hi = sw ? b : a, lo = sw ? a : b;
+  a = hi;
+  b = lo;
+}
+template <int N>
+__device__ __forceinline__ void bitonic_desc64(uint64_t (&v)[N]) {
+#pragma unroll
+  for (int k = 2; k <= N; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const int l = i ^ j;
+        if (l > i) {
+          if ((i & k) == 0)
+            cx_desc64(v[i], v[l]);
+          else
+            cx_desc64(v[l], v[i]);
+        }
+      }
+}
+template <int KL>
+__device__ __forceinline__ void fold_sorted(const v4i32 (&a)[4], float st, int rbase, uint32_t pm, uint64_t (&L)[KL],
+                                            uint32_t& drop_o) {
+  static_assert(KL <= 16, "one 16-key merge");
+  uint64_t K[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float s = (float)a[r >> 2][r & 3] * st;
+    const int row = rbase + (r & 7) + 16 * (r >> 3);
+    const uint64_t key = ((uint64_t)ord(s) << 32) | (uint32_t)(~(uint32_t)row);
+    K[r] = (pm >> r) & 1u ? key : 0ull;
+  }
+  bitonic_desc64<16>(K);
+  uint64_t M[16];
+  uint32_t d = KL < 16 ? (uint32_t)(K[KL] >> 32) : 0u;
+#pragma unroll
+  for (int i = 0; i < KL; ++i) {
+    const uint64_t x = L[i], y = K[KL - 1 - i];
+    M[i] = x > y ? x : y;
+    const uint64_t lo = x > y ? y : x;
+    d = max(d, (uint32_t)(lo >> 32));
+  }
+#pragma unroll
+  for (int i = KL; i < 16; ++i) M[i] = 0ull;  // (constant: the network folds them away)
+  bitonic_desc64<16>(M);
+#pragma unroll
+  for (int i = 0; i < KL; ++i) L[i] = M[i];
+  drop_o = max(drop_o, d);
+}
+constexpr int kSortMergeTrips = 8;  // (a merge costs about as much VALU as 8 trips)
+template <int KL, bool REG = true, bool FMASK = false, bool SORTM = false>
 __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint32_t bits, uint64_t* Ls, uint64_t (&L)[KL],
                                             uint32_t& thr_o,
                                             float e2, uint32_t& drop_o, int rbase, v4i32 tau_rsrc, uint32_t slot_voff) {
   if constexpr (REG) {
     bool pub;
     uint32_t pm = FMASK ? fold_mask(a, st, bits, thr_o, e2, pub) : fold_mask_int(a, st, bits, thr_o, e2, pub);
-    // one passing value per lane per trip: the wave makes max-over-lanes(popcount) trips, not one
-    // trip per position some lane passes at
-    while (pm) fold_trip<KL>(a, st, rbase, pm, L, drop_o);
+    int many = 0;
+    if constexpr (SORTM) {  // the wave's largest pass count: one sorted merge when it is high
+      int c = __popc(pm);
+#pragma unroll
+      for (int off = 32; off; off >>= 1) c = max(c, __shfl_xor(c, off));
+      many = c >= kSortMergeTrips;
+    }
+    if (SORTM && many) {
+      fold_sorted<KL>(a, st, rbase, pm, L, drop_o);
+    } else {
+      // one passing value per lane per trip: the wave makes max-over-lanes(popcount) trips, not one
+      // trip per position some lane passes at
+      while (pm) fold_trip<KL>(a, st, rbase, pm, L, drop_o);
+    }
     fold_end<KL>(L, thr_o, pub, tau_rsrc, slot_voff);
   } else {
     const float thr = thr_o ? unord(thr_o) - e2 : -__builtin_inff();
@@ -387,6 +457,7 @@ constexpr int kModePermBounds = 524288;
 constexpr int kModeFold2 = 1048576;  // the round-5 u32-score fold (debug; slower, see above)
 constexpr int kModeTileBarrier = 2097152;  // one wait + barrier per tile (TB below; RING 12)
 constexpr int kModeFloatMask = 4194304;  // the slow path's float pass mask (fold_mask) instead of fold_mask_int
+constexpr int kModeSortMerge = 16384;  // a wave with >= 8 passes in some lane folds by one sorted merge (debug)
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
@@ -729,7 +800,8 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
             batomic_umax(tau_rsrc, slot_voff, LS[0]);
           }
         } else {
-          fold_screen<KL, (MODE & 1024) == 0, (MODE & kModeFloatMask) != 0>(acc4, st, lw >> (8 * half), Ls, Lr, thr, e2, drop,
+          fold_screen<KL, (MODE & 1024) == 0, (MODE & kModeFloatMask) != 0, (MODE & kModeSortMerge) != 0>(
+              acc4, st, lw >> (8 * half), Ls, Lr, thr, e2, drop,
                                                                               tile * kTM + 8 * half,
                                               tau_rsrc, slot_voff);
         }
