@@ -28,7 +28,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt3
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kts -o kts -- python $R/bench.py $CS > $O/bench_kts.log 2>&1 || { tail -20 $O/bench_kts.log; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt2 -o kt2 -- python $R/bench.py $C2 > $O/bench_kt2.log 2>&1 || { tail -20 $O/bench_kt2.log; exit 1; }
 P3="--steps 4 --warmup 1 --no-cpu-baseline --oracle-stride 0"
-PS="--rows 1250000 --force-comm --steps 20 --warmup 2 --no-cpu-baseline --oracle-stride 0"
+Ps="--rows 1250000 --force-comm --steps 20 --warmup 2 --no-cpu-baseline --oracle-stride 0"
 P2="--rows 100000 --dtype f32 --nq 1 --steps 200 --warmup 20 --no-cpu-baseline --oracle-stride 0"
 for c in 3 s 2; do
   eval P=\$P$c
