@@ -10,8 +10,9 @@
 // inserts in tiles 0-1; slower, not production), 2097152 one wait + barrier per tile (RING 10 / 12; production
 // at RING 10), 4194304 the slow path's float pass mask instead of the integer threshold, 16384 a sorted
 // merge instead of the pop loop when some lane passes >= 8 values (round 5),
-// via rfx_dbg_screen_variant; variant = 10^7 * RING + MODE (RING in {4, 6, 8, 10, 12}; rounds 3-4 used
-// 100000 * RING + MODE).
+// 8388608 a list's best published only when it rose (round 5),
+// via rfx_dbg_screen_variant; variant = 10^8 * RING + MODE (RING in {4, 6, 8, 10, 12}; round 5's first
+// sessions used 10^7 * RING + MODE, rounds 3-4 100000 * RING + MODE).
 #define RFX_K10_BLOCK_TIMES
 #include "k_scan_screen.h"
 
@@ -25,7 +26,7 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
   const int ntiles = (nrows + k10::kTM - 1) / k10::kTM;
   dim3 grid(p.blocks, p.q_blocks);
 #define RFX_K10V(R, M)                                                                                        \
-  case 10000000 * R + M:                                                                                          \
+  case 100000000 * R + M:                                                                                          \
     hipLaunchKernelGGL((k10::scan_screen_kernel<10, 768, false, R, M>), grid, dim3(512), 0, st, X, tm, sts, Qc, \
                        qe2, nq, ntiles, tau, cs, cr, dr, p.n_lists, nullptr, tau + p.nq_pad * k10::kTauW,      \
                        xcd_weights_device_ptr());                                                             \
@@ -60,6 +61,10 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
     RFX_K10V(10, 2097152 + 4194304 + 8192)
     RFX_K10V(10, 2097152 + 16384)
     RFX_K10V(10, 2097152 + 16384 + 8192)
+    RFX_K10V(10, 2097152 + 8388608)
+    RFX_K10V(10, 2097152 + 8388608 + 8192)
+    RFX_K10V(10, 2097152 + 8388608 + 512)
+    RFX_K10V(10, 2097152 + 8388608 + 1)
     RFX_K10V(12, 2097152 + 1)
     RFX_K10V(12, 2097152 + 512)
     default:

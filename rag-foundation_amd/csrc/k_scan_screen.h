@@ -253,13 +253,20 @@ __device__ __forceinline__ void fold_trip(const v4i32 (&a)[4], float st, int rba
   L[0] = c[0] ? L[0] : key;
   drop_o = max(drop_o, (uint32_t)(k >> 32));
 }
-template <int KL>
+// PUBCH (kModePubOnChange, production since round 5): the list's best is published only when it rose above what this lane
+// published last (the slot table holds the same values either way: an atomic max with a value already
+// published is a no-op), so a slow-path entry that does not raise the list's best issues no atomic.
+template <int KL, bool PUBCH = false>
 __device__ __forceinline__ void fold_end(const uint64_t (&L)[KL], uint32_t& thr_o, bool pub, v4i32 tau_rsrc,
-                                         uint32_t slot_voff) {
+                                         uint32_t slot_voff, uint32_t& pubd) {
   if (pub) {
     const uint32_t own = (uint32_t)(L[KL - 1] >> 32);
     thr_o = own > thr_o ? own : thr_o;
-    batomic_umax(tau_rsrc, slot_voff, (uint32_t)(L[0] >> 32));
+    const uint32_t best = (uint32_t)(L[0] >> 32);
+    if (!PUBCH || best > pubd) {
+      batomic_umax(tau_rsrc, slot_voff, best);
+      pubd = best;
+    }
   }
 }
 // Debug kModeSortMerge (round 5): a wave whose lanes pass many values at once (the first tiles, where
@@ -321,10 +328,11 @@ __device__ __forceinline__ void fold_sorted(const v4i32 (&a)[4], float st, int r
   drop_o = max(drop_o, d);
 }
 constexpr int kSortMergeTrips = 8;  // (a merge costs about as much VALU as 8 trips)
-template <int KL, bool REG = true, bool FMASK = false, bool SORTM = false>
+template <int KL, bool REG = true, bool FMASK = false, bool SORTM = false, bool PUBCH = false>
 __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint32_t bits, uint64_t* Ls, uint64_t (&L)[KL],
                                             uint32_t& thr_o,
-                                            float e2, uint32_t& drop_o, int rbase, v4i32 tau_rsrc, uint32_t slot_voff) {
+                                            float e2, uint32_t& drop_o, int rbase, v4i32 tau_rsrc, uint32_t slot_voff,
+                                            uint32_t& pubd) {
   if constexpr (REG) {
     bool pub;
     uint32_t pm = FMASK ? fold_mask(a, st, bits, thr_o, e2, pub) : fold_mask_int(a, st, bits, thr_o, e2, pub);
@@ -342,7 +350,7 @@ __device__ __forceinline__ void fold_screen(const v4i32 (&a)[4], float st, uint3
       // trip per position some lane passes at
       while (pm) fold_trip<KL>(a, st, rbase, pm, L, drop_o);
     }
-    fold_end<KL>(L, thr_o, pub, tau_rsrc, slot_voff);
+    fold_end<KL, PUBCH>(L, thr_o, pub, tau_rsrc, slot_voff, pubd);
   } else {
     const float thr = thr_o ? unord(thr_o) - e2 : -__builtin_inff();
 #pragma unroll
@@ -457,6 +465,7 @@ constexpr int kModePermBounds = 524288;
 constexpr int kModeFold2 = 1048576;  // the round-5 u32-score fold (debug; slower, see above)
 constexpr int kModeTileBarrier = 2097152;  // one wait + barrier per tile (TB below; RING 12)
 constexpr int kModeFloatMask = 4194304;  // the slow path's float pass mask (fold_mask) instead of fold_mask_int
+constexpr int kModePubOnChange = 8388608;  // publish a list's best only when it rose (production; variant encoding 10^8 RING + MODE)
 constexpr int kModeSortMerge = 16384;  // a wave with >= 8 passes in some lane folds by one sorted merge (debug)
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
@@ -591,6 +600,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   };
 
   uint32_t thr = 0u, drop = 0u;
+  uint32_t pubd = 0u;  // the list's best this lane published last (kModePubOnChange)
   // Debug MODE 64's fast path, bounds on the raw i32 dot D (no per-tile data): every tile scale s_t <= smax, so a
   // lane value with D < ibound(thr) has fl(D s_t) < thr - e2 and is never looked at (proof in
   // DESIGN §4.10).  ti_own: this lane's query (after the pair swap); ti_oth: the query the partner
@@ -800,10 +810,11 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
             batomic_umax(tau_rsrc, slot_voff, LS[0]);
           }
         } else {
-          fold_screen<KL, (MODE & 1024) == 0, (MODE & kModeFloatMask) != 0, (MODE & kModeSortMerge) != 0>(
+          fold_screen<KL, (MODE & 1024) == 0, (MODE & kModeFloatMask) != 0, (MODE & kModeSortMerge) != 0,
+                      (MODE & kModePubOnChange) != 0>(
               acc4, st, lw >> (8 * half), Ls, Lr, thr, e2, drop,
                                                                               tile * kTM + 8 * half,
-                                              tau_rsrc, slot_voff);
+                                              tau_rsrc, slot_voff, pubd);
         }
         set_bounds();
         if constexpr ((MODE & 2048) != 0) __builtin_amdgcn_s_setprio(0);
@@ -1001,8 +1012,10 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
 // against round 4's wait + barrier per stage over 8 slots: 2.004 against 2.054 ms at 10M rows, 0.3313 against
 // 0.3393 ms at the 8-GPU shard (one box, interleaved, profiles/r05/k10_tb_ab_*.txt); round 4's schedule stays
 // in the debug library as variant (8, 0).
+// Production publishes a list's best only when it rose (kModePubOnChange: the same slot table, fewer
+// atomics): 0.3344 against 0.3461 ms at the shard, 2.039 against 2.038 ms at 10M (profiles/r05/k10_pub_ab_*.txt).
 constexpr int kProdRing = 10;
-constexpr int kProdMode = kModeTileBarrier;
+constexpr int kProdMode = kModeTileBarrier | kModePubOnChange;
 // one translation unit per D instantiates the kernel for KL in {4, 10}, with and without a filter mask
 #define RFX_K10_INSTANTIATE(DV, NAME)                                                                         \
   int NAME(int kl, dim3 grid, hipStream_t st, const int8_t* X, const uint4* tm, const uint32_t* sts,           \

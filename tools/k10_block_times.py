@@ -24,7 +24,7 @@ ap.add_argument("--rows", type=int, default=1_250_000)
 ap.add_argument("--nq", type=int, default=256)
 ap.add_argument("--k", type=int, default=10)
 ap.add_argument("--reps", type=int, default=20)
-ap.add_argument("--variant", type=int, default=80065536, help="80065536 = production split + clocks; 80069632 = static split")
+ap.add_argument("--variant", type=int, default=800065536, help="800065536 = round 4 schedule + clocks; 800069632 = static split (10**8 * RING + MODE)")
 a = ap.parse_args()
 f = _lib.lib.rfx_dbg_screen_variant
 f.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,

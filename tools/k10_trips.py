@@ -21,7 +21,7 @@ from rfx.index import DeviceIndex, synth_rows  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--rows", type=int, default=1_250_000)
 ap.add_argument("--reps", type=int, default=5)
-ap.add_argument("--variant", type=int, default=80008192, help="a MODE-8192 variant (10**7 * RING + MODE)")
+ap.add_argument("--variant", type=int, default=1010493952, help="a MODE-8192 variant (10**8 * RING + MODE; production + 8192 by default)")
 a = ap.parse_args()
 f = _lib.lib.rfx_dbg_screen_variant
 f.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,

@@ -2,7 +2,7 @@
 corpus in bursts of back-to-back launches, variants interleaved over rounds (the chip's clock
 settles per workload; cdna_hip_programming.md §5.4 rule 24).
 
-variant = 10**7 * RING + MODE (k10_dbg.hip; round 4's logs used 100000 * RING + MODE, round 3's 1000 * RING + MODE): RING in {4, 6, 8, 10, 12}; MODE 1 = no top-k fold,
+variant = 10**8 * RING + MODE (k10_dbg.hip; round 5 first used 10**7 * RING + MODE, round 4 100000 * RING + MODE, round 3 1000 * RING + MODE): RING in {4, 6, 8, 10, 12}; MODE 1 = no top-k fold,
 8 = no corpus stream after the prologue, 9 = both; 32 = count slow-path entries (reported, not
 timed); 64 = the store-wide integer fast-path bound."""
 import argparse
@@ -26,7 +26,7 @@ ap.add_argument("--nq", type=int, default=256)
 ap.add_argument("--k", type=int, default=10)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--burst", type=int, default=30)
-ap.add_argument("--variants", default="80000000,80000001,80000009,40000000")
+ap.add_argument("--variants", default="1010485760,800000000,1010485761,1010486272")
 ap.add_argument("--seconds", type=float, default=0.0, help="one variant back to back for this long (power sampling)")
 ap.add_argument("--validate", action="store_true", help="each variant's two-pass answer must equal production's")
 a = ap.parse_args()
