@@ -203,3 +203,50 @@ def test_union_cache_stays_within_its_byte_budget(tmp_path, monkeypatch):
     ret.union = True
     a = _hits(ret, names[:3], "roofline lds", 8)
     assert ret.last_path == "per-store"
+
+
+def test_single_store_question_while_a_union_builds(tmp_path, monkeypatch):
+    """a union view is built outside the process-wide _STATE_LOCK. A thread builds the
+    view of a 1,000,000-row store and a small one (held inside the build, between its first member copy
+    and the rest); meanwhile a single-store question through the same retriever completes."""
+    import threading
+
+    from rfx import retriever as rret
+    from rfx import store as rstore
+    from rfx import union as runion
+    from rfx.index import synth_rows
+    from rfx.retriever import GpuRetriever
+
+    reg = rstore.StoreRegistry(root=str(tmp_path), device=0)
+    ret = GpuRetriever(registry=reg, dtype="bf16")
+    ret.batching = False
+    small, big = ret.create_store("small"), ret.create_store("big")
+    for t, m in DOCS:
+        ret.add_document(small, t, "d", WS, m)
+    n_big = 1_000_000
+    reg.get(big).add_document(["c"] * n_big, synth_rows(5, 0, n_big, 768, "bf16", device=0), "bulk")
+    want = _hits(ret, [small], "alpha gamma", 5)
+    started, release = threading.Event(), threading.Event()
+    orig = runion.UnionView._copy
+
+    def held_copy(self, *a, **kw):  # the first member copy of the build waits for the question below
+        if not started.is_set():
+            started.set()
+            assert release.wait(60)
+        return orig(self, *a, **kw)
+
+    monkeypatch.setattr(runion.UnionView, "_copy", held_copy)
+    out = {}
+    stores = [reg.get(big), reg.get(small)]
+    t = threading.Thread(target=lambda: out.setdefault("v", ret._union_view([big, small], stores)))
+    t.start()
+    try:
+        assert started.wait(60)
+        got = _hits(ret, [small], "alpha gamma", 5)  # the build is in progress (and blocked)
+        assert got == want and t.is_alive()
+    finally:
+        release.set()
+        t.join(120)
+    v = out["v"]
+    assert v.rows == [n_big, reg.get(small).index.rows]
+    rret._release_union(v)
