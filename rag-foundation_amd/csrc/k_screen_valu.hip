@@ -171,6 +171,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   // NB row buffers: NB - 1 iterations of loads in flight ahead of the one being scored (one wave per
   // SIMD has nothing else to hide the latency; 3 in flight measured latency-bound at 2.6 TB/s)
   constexpr int NB = NQT == 1 ? 8 : 4;
+  static_assert(NB % 4 == 0, "the offer step takes whole 4-iteration groups (64-row chunks)");
   Codes<D> buf[NB];
   // The quantiser's inputs are requested first (the store maxima and this wave's first query, loaded
   // unconditionally: a load under a wave-uniform condition becomes a branch around it, and the join after

@@ -571,9 +571,14 @@ struct K11Order {
   hipEvent_t ev = nullptr;
   hipStream_t last = nullptr;
   bool used = false;
-  bool multi = false;     // a second stream has issued kernel 11 on this device
+  bool multi = false;     // a second stream has issued kernel 11 on this device recently
   bool recorded = false;  // ev holds the previous launch
+  int same = 0;           // launches in a row from the last stream (kK11OrderDecay of them end `multi`)
 };
+// after this many kernel-11 launches in a row from one stream the device goes back to recording
+// nothing (a process that once searched from two streams does not pay an event per search forever;
+// the next second-stream launch re-enables the order, and is correct without it)
+constexpr int kK11OrderDecay = 256;
 K11Order& k11_order(int device) {
   static K11Order o[64];
   return o[device & 63];
@@ -1420,7 +1425,11 @@ int search_impl(rfx_index_t h, const void* queries_d, int64_t nq, int k, const u
     if (!ko.ev) RFX_HIP(hipEventCreateWithFlags(&ko.ev, hipEventDisableTiming));
     if (ko.used && ko.last != st) {
       ko.multi = true;
+      ko.same = 0;
       if (ko.recorded && !k11_unordered()) RFX_HIP(hipStreamWaitEvent(st, ko.ev, 0));
+    } else if (ko.multi && ++ko.same >= kK11OrderDecay) {
+      ko.multi = false;
+      ko.recorded = false;
     }
     if ((rc = mark(ev0))) return rc;
     // one launch for a lone question: the screen, and the exact one-launch search run by the same
