@@ -16,8 +16,12 @@
 //     records' best entries (a lower bound of a_k: distinct live rows).  If some drop bound
 //     reaches a_k' - e2 a dropped row might belong to the top-k: not proven, and the exact search
 //     rewrites the answer.  Otherwise every row with
-//     A >= a_k' - e2 (the top-k among them, as a_k' <= a_k) is in a record: it re-scores those survivors exactly (f64 sum of the
-//     exact products, rounded to f32, 16 lanes per row) and ranks them (score desc, row asc).
+//     A >= a_k' - e2 (the top-k among them, as a_k' <= a_k) is in a record, and it ranks those
+//     survivors by their exact scores (f64 sum of the exact products, rounded to f32, 16 lanes per
+//     row; score desc, row asc).  The exact scores come with the records: each block re-scores the
+//     entries that can still survive before it arrives (its own k-th best A and the best such bound
+//     other blocks posted so far bound a_k' from below; step 3), so the re-score's memory round trip
+//     leaves the last block's critical path (round 5).
 // No atomics on shared addresses besides the arrival counter: the bound travels in the records.
 // The fallback inside the launch (lone question): the blocks that arrived before the last one wait, for
 // a bounded time, for its verdict; on "not proven" every block still there, and the last block itself,
@@ -62,6 +66,20 @@ struct Codes {
   uint4 v[C];
   uint4 md;  // the row's tile record {scale, live word}, loaded with the codes (prefetched alike)
 };
+
+// The two-pass score rule's exact dot of one row against one question, 16 lanes of a DPP row (chunk
+// gl + 16 u of each): the f64 sum of the exact products, lane 0 of the row holding the row's sum.  One
+// function for the blocks' re-score and the last block's, so their keys are bit-identical.
+template <int DT, int VPL>
+__device__ __forceinline__ double exact_dot16(const uint4 (&xv)[VPL], const uint4 (&yv)[VPL]) {
+  constexpr int EPV = DT == RFX_F32 ? 4 : 8;
+  double acc = 0.0;
+#pragma unroll
+  for (int u = 0; u < VPL; ++u)
+#pragma unroll
+    for (int ee = 0; ee < EPV; ++ee) acc += (double)elem<DT>(xv[u], ee) * (double)elem<DT>(yv[u], ee);
+  return row16_sum_f64(acc);  // (DPP; lane 0's sum = the xor butterfly's)
+}
 
 #ifdef RFX_DEBUG_BUILD
 // debug library only: the 100-MHz wall clock per block (< 1024) at 0 start, 1 query quantised, 2 row
@@ -117,7 +135,8 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
                                                           const void* __restrict__ X, const void* __restrict__ Q, int nq,
                                                           int rows_per_wave, const uint32_t* __restrict__ mask,
                                                           uint32_t* __restrict__ state, float* __restrict__ cand_s,
-                                                          int* __restrict__ cand_r, int k_out, float* __restrict__ out_s,
+                                                          int* __restrict__ cand_r, uint32_t* __restrict__ cand_x,
+                                                          int k_out, float* __restrict__ out_s,
                                                           int64_t* __restrict__ out_r, int force,
                                                           uint32_t* __restrict__ vtau, uint32_t* __restrict__ vctr) {
   constexpr int C = D / 256;
@@ -341,6 +360,8 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   // better than its own — a one-compare-per-entry rank, no serial insert loop.
   __shared__ uint64_t mk[NQT][4 * kK];
   __shared__ float wdm[4][NQT];
+  __shared__ int xrow[NQT][kK];  // per query: the rows this block re-scores early (record entries 0..nxl-1)
+  __shared__ int nxl[NQT];
 #pragma unroll
   for (int qi = 0; qi < NQT; ++qi) {
     if (lane < kK) {
@@ -379,7 +400,52 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       __hip_atomic_store((uint32_t*)cand_s + o0 + lane, __float_as_uint(d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(cand_r + o0 + lane, kDropRow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    // Early re-score (round 5).  LB_b = the block's k-th best A (record entry k - 1) is a lower bound of
+    // a_k (distinct live rows); the last block's bound LB* includes every record's entry k - 1 (k <= 15),
+    // so an entry it keeps has A >= LB* - e2 >= LB_b - e2 (f32 subtraction is monotone).  Those entries (a
+    // prefix of the ranks: A falls with the rank) are re-scored exactly by this block AFTER it arrives (off
+    // the critical path; step 4), their keys going to cand_x, which holds 0 for every entry until then.
+    // The last block takes a survivor's key from there, and re-scores a survivor whose key is still 0
+    // itself (its own entries, a block not done yet): no answer depends on the timing.
+    const uint64_t kb = __ballot(v && rank == k_out - 1);
+    const uint32_t lbb = kb ? ord_f32(readlane_f(ms_, (int)__builtin_ctzll(kb))) : 0u;
+    const float cutb = lbb ? unord_f32(lbb) - e2_lds[qi] : -__builtin_inff();
+    const bool rx = v && rank < kK - 1 && ms_ >= cutb;
+    if (v && rank < kK - 1) __hip_atomic_store(cand_x + o0 + rank, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane >= nv && lane < kK - 1) __hip_atomic_store(cand_x + o0 + lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (rx) xrow[qi][rank] = (int)(~(uint32_t)mine);
+    const int nx = (int)__popcll(__ballot(rx));
+    if (lane == 0) nxl[qi] = nx;
   }
+  // the early re-score (a block that is not the last, after it arrived): the entries above, 16 lanes each
+  // (the last block's layout), all queries' entries in a row
+  auto early_rescore = [&]() {
+    int tot = 0;
+    for (int qi = 0; qi < nq; ++qi) tot += nxl[qi];
+    tot = __builtin_amdgcn_readfirstlane(tot);
+    constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
+    constexpr int VPL = D * ESZ / 256;
+    const int grp = tid >> 4, gl = tid & 15;
+    for (int p0 = 0; p0 < tot; p0 += 16) {
+      const int p = p0 + grp < tot ? p0 + grp : 0;  // (clamped: whole 16-lane rows take part in the sum)
+      int qi = 0, e = p;
+      while (qi < nq - 1 && e >= nxl[qi]) {
+        e -= nxl[qi];
+        ++qi;
+      }
+      const int r = xrow[qi][e];
+      uint4 yv[VPL], xv[VPL];
+#pragma unroll
+      for (int u = 0; u < VPL; ++u) {
+        yv[u] = *(const uint4*)((const uint8_t*)Q + (int64_t)qi * D * ESZ + (int64_t)(gl + 16 * u) * 16);
+        xv[u] = *(const uint4*)((const uint8_t*)X + (int64_t)r * D * ESZ + (int64_t)(gl + 16 * u) * 16);
+      }
+      const double acc = exact_dot16<DT, VPL>(xv, yv);
+      if (gl == 0 && p0 + grp < tot)
+        __hip_atomic_store(cand_x + ((int64_t)qi * n_lists + blockIdx.x) * kK + e, ord_f32((float)acc),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
 
   // ---- 4. the last block: a_k from the records, the drop check, survivors, exact re-score, top-k --
   __shared__ int last;
@@ -392,6 +458,7 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   __syncthreads();
   RFX_K11_T(3);
   const bool lastu = __builtin_amdgcn_readfirstlane(last) != 0;  // (uniform: see fallback above)
+  if (!lastu && !(force & 16)) early_rescore();
   if (!INL && !lastu) return;
   if (!lastu) {
     // wait for the last block's verdict on this launch, at most kVerdictWait of wall clock (100 MHz):
@@ -428,11 +495,13 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   __shared__ float bs[kFusedLdsCand];
   __shared__ int br[kFusedLdsCand];
   __shared__ int sv[kSurvCap];    // survivor -> record index
+  __shared__ int mv[kSurvCap];    // survivors without an exact key (re-scored here)
   // its rank key: (orderable fl32 of the exact f64 sum) << 32 | ~row, larger = better under (score
   // desc, row asc): the rank is one 64-bit compare per survivor (no branches, no dependent LDS loads)
   __shared__ uint64_t skey[kSurvCap];
   __shared__ float red[4];
-  __shared__ int n_sv, fail;
+  __shared__ uint32_t redg[4];
+  __shared__ int n_sv, n_mv, fail;
   __shared__ float cut;
   __shared__ uint32_t fin[4 * kK];
   if (tid == 0) fail = force & 1;
@@ -460,7 +529,10 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
         }
       }
     }
-    if (tid == 0) n_sv = 0;
+    if (tid == 0) {
+      n_sv = 0;
+      n_mv = 0;
+    }
     __syncthreads();
     if (qi == 0) RFX_K11_L(1);
     // The largest drop bound (entry 15 of each record), and LB, a lower bound of a_k: the k-th largest
@@ -469,12 +541,19 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     // (4 per lane, sorted in registers) by k rounds of a wave max; wave 0 ranks the 4k finalists (the
     // union of the waves' top-k holds the top-k values with their multiplicity).
     float dmax = -__builtin_inff();
+    uint32_t gk = 0u;  // the largest block bound LB_b (record entry k - 1; k <= 15)
     for (int c = tid; c < n_lists; c += 256) {
       const int i = c * kK + kK - 1;
       if (br[i] == kDropRow) dmax = fmaxf(dmax, bs[i]);
+      const int i2 = c * kK + k_out - 1, r2 = br[i2];
+      if (k_out < kK && r2 != kEmptyRow && r2 != kDropRow) gk = max(gk, ord_f32(bs[i2]));
     }
     dmax = wave_max_f32(dmax);
-    if (lane == 0) red[w] = dmax;
+    gk = wave_max_u32(gk);
+    if (lane == 0) {
+      red[w] = dmax;
+      redg[w] = gk;
+    }
     const bool every = n <= 1024;
     const int m = (force & 32) ? 0 : every ? n : n_lists;  // <= 1024
     {
@@ -525,7 +604,8 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
         gt += v > x ? 1 : 0;
       }
       uint32_t lb = x && gt < k_out && ge >= k_out ? x : 0u;
-      lb = wave_max_u32(lb);
+      // LB* = the larger of the two lower bounds of a_k: >= every LB_b the blocks re-scored against
+      lb = max(wave_max_u32(lb), max(max(redg[0], redg[1]), max(redg[2], redg[3])));
       if (lane == 0) {
         const float dm_all = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
         cut = lb ? unord_f32(lb) - e2_lds[qi] : -__builtin_inff();
@@ -552,39 +632,49 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     if (qi == 0) RFX_K11_L(3);
     if (!fail && !(force & 16)) {
       const int ns = n_sv;
-      // exact re-score: 16 lanes per survivor (16-B chunks gl + 16 u of the row), UR survivors per group
-      // in flight, 32 per round (config 2: ~30 survivors, one round = one memory latency); the query's
-      // chunks are loaded once per query, not per survivor
-      constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
-      constexpr int EPV = 16 / ESZ;
-      constexpr int VPL = D * ESZ / 256;
-      constexpr int UR = 2;
-      const int grp = tid >> 4, gl = tid & 15;
-      uint4 yv[VPL];
+      // the survivors' exact keys from the blocks' early re-score (one round of loads), read now, when
+      // the blocks that arrived before this one have had the bound, drop check and survivors' time to
+      // write them; a key still 0 (this block's own entries, a block not done yet) is re-scored here
+      for (int e = tid; e < ns; e += 256) {
+        const int i = sv[e];
+        const uint32_t x = __hip_atomic_load(cand_x + (int64_t)qi * n + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (x)
+          skey[e] = ((uint64_t)x << 32) | (uint32_t)(~(uint32_t)br[i]);
+        else
+          mv[atomicAdd(&n_mv, 1)] = e;
+      }
+      __syncthreads();
+      // exact re-score of those: 16 lanes per survivor (16-B chunks gl + 16 u of the row), UR survivors per group
+      // in flight, 32 per round; the query's chunks are loaded once per query, not per survivor
+      const int nm = __builtin_amdgcn_readfirstlane(n_mv);
+      if (nm > 0) {
+        constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
+        constexpr int VPL = D * ESZ / 256;
+        constexpr int UR = 2;
+        const int grp = tid >> 4, gl = tid & 15;
+        uint4 yv[VPL];
 #pragma unroll
-      for (int u = 0; u < VPL; ++u)
-        yv[u] = *(const uint4*)((const uint8_t*)Q + (int64_t)qi * D * ESZ + (int64_t)(gl + 16 * u) * 16);
-      for (int e0 = 0; e0 < ns; e0 += 16 * UR) {
-        uint4 xv[UR][VPL];
+        for (int u = 0; u < VPL; ++u)
+          yv[u] = *(const uint4*)((const uint8_t*)Q + (int64_t)qi * D * ESZ + (int64_t)(gl + 16 * u) * 16);
+        for (int e0 = 0; e0 < nm; e0 += 16 * UR) {
+          uint4 xv[UR][VPL];
 #pragma unroll
-        for (int ur = 0; ur < UR; ++ur) {
-          const int e = e0 + grp + 16 * ur;
-          const int r = br[sv[e < ns ? e : 0]];
+          for (int ur = 0; ur < UR; ++ur) {
+            const int e = e0 + grp + 16 * ur;
+            const int r = br[sv[mv[e < nm ? e : 0]]];
 #pragma unroll
-          for (int u = 0; u < VPL; ++u)
-            xv[ur][u] = *(const uint4*)((const uint8_t*)X + (int64_t)r * D * ESZ + (int64_t)(gl + 16 * u) * 16);
-        }
+            for (int u = 0; u < VPL; ++u)
+              xv[ur][u] = *(const uint4*)((const uint8_t*)X + (int64_t)r * D * ESZ + (int64_t)(gl + 16 * u) * 16);
+          }
 #pragma unroll
-        for (int ur = 0; ur < UR; ++ur) {
-          const int e = e0 + grp + 16 * ur;
-          double acc = 0.0;
-#pragma unroll
-          for (int u = 0; u < VPL; ++u)
-#pragma unroll
-            for (int ee = 0; ee < EPV; ++ee) acc += (double)elem<DT>(xv[ur][u], ee) * (double)elem<DT>(yv[u], ee);
-          acc = row16_sum_f64(acc);  // within the 16-lane group (DPP; lane 0's sum = the xor butterfly's)
-          if (gl == 0 && e < ns)
-            skey[e] = ((uint64_t)ord_f32((float)acc) << 32) | (uint32_t)(~(uint32_t)br[sv[e]]);
+          for (int ur = 0; ur < UR; ++ur) {
+            const int e = e0 + grp + 16 * ur;
+            const double acc = exact_dot16<DT, VPL>(xv[ur], yv);
+            if (gl == 0 && e < nm) {
+              const int jj = mv[e];
+              skey[jj] = ((uint64_t)ord_f32((float)acc) << 32) | (uint32_t)(~(uint32_t)br[sv[jj]]);
+            }
+          }
         }
       }
       __syncthreads();
@@ -642,8 +732,9 @@ int dbg_k11_times(unsigned long long* blocks_h, unsigned long long* last_h) {
 // vstate: bounds, then counters).
 int launch_screen_valu(const ValuPlan& p, const int8_t* X8, const void* tmeta, const uint32_t* stats, int nrows, int D,
                        int dtype, const void* X, const void* Q, int nq, const uint32_t* mask, uint32_t* state,
-                       uint32_t* vstate, float* cs, int* cr, int k, float* out_s, int64_t* out_r, int force,
-                       hipStream_t st) {
+                       uint32_t* vstate, float* cs, int* cr, uint32_t* cx, int k, float* out_s, int64_t* out_r,
+                       int force, hipStream_t st) {
+  if (!cx) return -1;
   if (nq < 1 || nq > 8 || k < 1 || k > kK || (D != 768 && D != 1024)) return -1;
   if ((int64_t)p.blocks * kK > (int64_t)1 << 30) return -1;
   if (screen_valu_inline_fallback(nq == 1 ? 1 : 8, dtype, D) && (!vstate || p.q_slices != 1 || valu_k_slot(k) != 16))
@@ -653,7 +744,7 @@ int launch_screen_valu(const ValuPlan& p, const int8_t* X8, const void* tmeta, c
   uint32_t* const vctr = vstate ? vstate + kValuFusedMaxNq : nullptr;
 #define RFX_SV(DTV, DV, NQ)                                                                                      \
   hipLaunchKernelGGL((screen_valu_kernel<DTV, DV, NQ>), grid, dim3(256), 0, st, X8, (const uint4*)tmeta, stats, nrows, \
-                     X, Q, nq, p.rows_per_wave, mask, state, cs, cr, k, out_s, out_r, force, vtau, vctr)
+                     X, Q, nq, p.rows_per_wave, mask, state, cs, cr, cx, k, out_s, out_r, force, vtau, vctr)
 #define RFX_SV_D(DTV)                  \
   if (D == 768) {                      \
     if (nq == 1)                       \

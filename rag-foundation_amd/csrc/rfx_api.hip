@@ -275,6 +275,9 @@ struct SearchLayout {
   // the one-launch VALU searches (kernel 11, the fused exact search) write (score, row) pairs: for a
   // records / row-offset output they go here first and one pack launch converts them (sharded stores)
   size_t pk_off, pk_r_off;
+  // kernel 11 (nq <= 8 on a VALU plan): the exact score keys of the record entries its blocks re-score
+  // before they arrive ([nq][blocks][16] u32, beside the records at cs_off / cr_off)
+  size_t cx_off;
 };
 
 size_t align_up(size_t x) { return (x + 255) / 256 * 256; }
@@ -393,6 +396,12 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L, bool search
     L.pk_off = L.total;
     L.pk_r_off = L.pk_off + align_up((size_t)nq * k * 4);
     L.total = L.pk_r_off + align_up((size_t)nq * k * 8);
+  }
+  L.cx_off = 0;
+  if (search && L.kernel == 0 && nq >= 1 && nq <= 8 && ix.rows > 0) {
+    // (whether or not the index holds an int8 copy yet: a workspace sized before enable_screen fits)
+    L.cx_off = L.total;
+    L.total = L.cx_off + align_up((size_t)nq * L.n_cand * 4);
   }
   return RFX_OK;
 }
@@ -591,7 +600,7 @@ bool k11_unordered() {
 }
 
 bool screen_valu_eligible(const Index& ix, const SearchLayout& L, int64_t nq, int k) {
-  return ix.screen && ix.rows > 0 && L.kernel == 0 && nq >= 1 && nq <= 8 && k <= 16 && L.vp.k_slot == 16 &&
+  return ix.screen && ix.rows > 0 && L.kernel == 0 && L.cx_off && nq >= 1 && nq <= 8 && k <= 16 && L.vp.k_slot == 16 &&
          rfx::screen_supported(ix.dim, ix.dtype) && fused_enabled();
 }
 
@@ -1435,7 +1444,8 @@ int search_impl(rfx_index_t h, const void* queries_d, int64_t nq, int k, const u
     // one launch for a lone question: the screen, and the exact one-launch search run by the same
     // launch when the screen cannot prove its answer (its state: the front of the same search state)
     if (rfx::launch_screen_valu(L.vp, ix->scodes, ix->smeta, ix->sstats, (int)ix->rows, ix->dim, ix->dtype, ix->data,
-                                queries_d, (int)nq, row_mask_d, sv, state, cs, cr, k, vo_s, vo_r,
+                                queries_d, (int)nq, row_mask_d, sv, state, cs, cr, (uint32_t*)(ws + L.cx_off), k,
+                                vo_s, vo_r,
                                 (ix->screen == 2 ? 1 : 0) | k11_ablate(), st) != 0)
       return fail(RFX_EUNSUPPORTED, "two-pass VALU search launch rejected");
     if (ko.multi) {

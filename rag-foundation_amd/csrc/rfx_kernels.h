@@ -56,14 +56,15 @@ int launch_search_valu_fused(const ValuPlan& p, const void* X, int nrows, int D,
 // index's int8 copy (codes X8, tile records tmeta, quantiser stats), the exact rows X / queries Q in
 // the index dtype; writes (out_s, out_r) and the fallback gate state[24] (state = the index's
 // per-stream search state + kScreenValuState, zero on entry and left zero except the gate and the
-// launch generation / verdict / claim words).  For a lone question (screen_valu_inline_fallback) the
+// launch generation / verdict / claim words).  cx: [nq][blocks][16] u32 workspace, the exact score keys
+// of the record entries (cs / cr) the blocks re-score.  For a lone question (screen_valu_inline_fallback) the
 // exact fallback runs INSIDE the launch when the screen cannot prove its answer (vstate = the
 // one-launch VALU search's state, the per-stream search state's base); otherwise the caller launches
 // the gated one-launch VALU search after it (launch_search_valu_fused with gate = state + 24).
 int launch_screen_valu(const ValuPlan& p, const int8_t* X8, const void* tmeta, const uint32_t* stats, int nrows, int D,
                        int dtype, const void* X, const void* Q, int nq, const uint32_t* mask, uint32_t* state,
-                       uint32_t* vstate, float* cs, int* cr, int k, float* out_s, int64_t* out_r, int force,
-                       hipStream_t st);
+                       uint32_t* vstate, float* cs, int* cr, uint32_t* cx, int k, float* out_s, int64_t* out_r,
+                       int force, hipStream_t st);
 constexpr bool screen_valu_inline_fallback(int nqt, int dtype, int D) {
   return nqt == 1 && !(dtype == RFX_F32 && D == 1024);  // (f32 at d 1024: the two bodies together spill)
 }
