@@ -647,6 +647,12 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       // exact re-score of those: 16 lanes per survivor (16-B chunks gl + 16 u of the row), UR survivors per group
       // in flight, 32 per round; the query's chunks are loaded once per query, not per survivor
       const int nm = __builtin_amdgcn_readfirstlane(n_mv);
+#ifdef RFX_DEBUG_BUILD
+      if (qi == 0 && tid == 0) {  // survivors, and those without a key from the blocks (tools/k11_phases.py)
+        g_k11_last[6] = (unsigned long long)ns;
+        g_k11_last[7] = (unsigned long long)nm;
+      }
+#endif
       if (nm > 0) {
         constexpr int ESZ = DT == RFX_F32 ? 4 : 2;
         constexpr int VPL = D * ESZ / 256;

@@ -4,7 +4,9 @@ copies, then reads the per-block phase clocks of the last launch (100-MHz wall c
 rfx_dbg_k11_times) and prints medians over the repetitions:
   per block (median / max over blocks): quantiser, row stream, block merge + record + arrival;
   the last block: records loaded, bound + drop check, survivors, re-score + rank, end;
-  span = last block's end - first block's start."""
+  span = last block's end - first block's start;
+  survivors of query 0 and how many of them had no exact key from the blocks' early re-score (the
+  last block re-scored those itself), median and the fraction of searches with any."""
 import argparse
 import ctypes
 import json
@@ -58,12 +60,13 @@ for rep in range(a.reps):
                  "merge_record_ns": [int(np.median(d[:, 2])), int(d[:, 2].max())],
                  "last_arrival_after_start_ns": int(b[:, 3].max() - t0),
                  "last_block_ns": [int(x) for x in np.diff(l[:6])],
-                 "span_ns": int(l[5] - t0)})
-keys = ["start_skew_ns", "last_arrival_after_start_ns", "span_ns"]
+                 "span_ns": int(l[5] - t0), "survivors": int(lt[6]), "missing_keys": int(lt[7])})
+keys = ["start_skew_ns", "last_arrival_after_start_ns", "span_ns", "survivors", "missing_keys"]
 med = {k: int(np.median([r[k] for r in recs[a.reps // 4:]])) for k in keys}
 for k in ["quant_ns", "stream_ns", "merge_record_ns", "last_block_ns"]:
     arr = np.array([r[k] for r in recs[a.reps // 4:]])
     med[k] = [int(x) for x in np.median(arr, axis=0)]
+med["searches_with_missing_keys"] = float(np.mean([r["missing_keys"] > 0 for r in recs[a.reps // 4:]]))
 print(json.dumps({"rows": a.rows, "dtype": a.dtype, "blocks": recs[-1]["blocks"], "median": med,
                   "last_block_phases": ["records loaded", "bound+drop check", "survivors", "re-score+rank", "end"]},
                  indent=1))
