@@ -186,10 +186,11 @@ def main():
     r0, r1 = rdist.shard_range(a.rows, rank, world)
     n_local = r1 - r0
     esz = {"bf16": 2, "f16": 2, "f32": 4}[a.dtype]
-    # the exact two-pass scan: kernel 10 for batches (bf16/f16, nq > 64, k <= 10), kernel 11 for a few
-    # questions (any dtype, nq <= 8, 5 <= k <= 16; config 2)
+    # the exact two-pass scan: kernel 10 for batches (nq > 8, k <= 10: the 2-wave kernel up to 64 questions, the
+    # 8-wave one above; bf16 / f16 at d 768 / 1024, f32 at d 768), kernel 11 for a few questions (any dtype,
+    # nq <= 8, 5 <= k <= 16; config 2)
     screen = a.scan == "auto" and a.dim in (768, 1024) and (
-        (a.dtype in ("bf16", "f16") and a.nq > 64 and a.k <= 10) or (a.nq <= 8 and 5 <= a.k <= 16))
+        (a.nq > 8 and a.k <= 10 and (a.dtype in ("bf16", "f16") or a.dim == 768)) or (a.nq <= 8 and 5 <= a.k <= 16))
     row_bytes = a.dim if screen else a.dim * esz  # what a scan streams per row
     copies = a.copies or min(8, max(1, -(-(768 << 20) // max(n_local * row_bytes, 1)) + 1))
     if copies > 1 and n_local * row_bytes > (1 << 30):
@@ -402,7 +403,14 @@ def main():
     n_max = rdist.shard_range(a.rows, 0, world)[1]
     nq_pad = -(-a.nq // 256) * 256
     if kern == 10:
-        n_lists = 2 * min(256 // max(1, nq_pad // 256), -(-n_max // 32))
+        ntiles = -(-n_max // 32)
+        if a.nq <= 64:  # the 2-wave kernel (k_screen.hip plan_scan_screen): 64 queries, up to 512 workgroups
+            nq_pad = 64
+            blocks = min(int(os.environ.get("RFX_SCREEN_W2_BLOCKS", "0")) or 512, max(ntiles // 8, 8))
+            blocks = max(min(blocks // 8 * 8 if blocks > 8 else blocks, ntiles), 1)
+        else:
+            blocks = min(256 // max(1, nq_pad // 256), ntiles)
+        n_lists = 2 * blocks
         kl = 4 if a.k <= 4 else 10
         alg_bytes = (n_max * a.dim + (-(-n_max // 32)) * 16 + nq_pad * a.dim + nq_pad * 4
                      + a.nq * n_lists * (kl * 8 + 4))

@@ -72,6 +72,17 @@ int rfx_init(int device);
 int rfx_index_create(int device, int dim, int dtype, int64_t capacity, rfx_index_t* out);
 /* Drops the store (delete_store gemini_rag.py:354-390). */
 int rfx_index_destroy(rfx_index_t h);
+/* A question over several stores (the file-search tool's list of store names, gemini_rag.py:463-469)
+ * as ONE index: a read-only view that maps the members' device memory back to back through HIP virtual
+ * memory (no copy).  Member m's rows are the view's rows [out_bases[m], out_bases[m] + its rows); the rest
+ * of its capacity is NaN (never returned).  The view's own device bytes are the tile records of the int8
+ * copy (16 B per 32 rows, copied) and 256 B of stats, when every member holds an int8 copy.  Appends and
+ * tombstones of the members show through; rfx_union_refresh copies their tile records again and sets
+ * *out_stale when a member moved its memory (growth, a rebuilt or dropped copy) or was destroyed: the
+ * caller then destroys the view (rfx_index_destroy) and creates a new one.  RFX_EUNSUPPORTED without
+ * virtual memory (RFX_VMM=0): the caller copies instead (rfx/union.py). */
+int rfx_union_create(const rfx_index_t* members, int n, void* stream, rfx_index_t* out, int64_t* out_bases);
+int rfx_union_refresh(rfx_index_t view, void* stream, int* out_stale);
 int rfx_index_info(rfx_index_t h, int* dim, int* dtype, int64_t* rows, int64_t* capacity,
                    int64_t* live_rows);
 int rfx_index_reserve(rfx_index_t h, int64_t capacity);

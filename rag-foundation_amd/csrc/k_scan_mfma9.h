@@ -82,7 +82,10 @@ __global__ __launch_bounds__(256, 1) void scan_mfma9_kernel(const float* __restr
                                                             int nq, int ntiles, int ranges, int groups, int paired,
                                                             uint32_t* __restrict__ tau, float* __restrict__ cand_s,
                                                             int* __restrict__ cand_r, int64_t n_lists,
-                                                            const uint32_t* __restrict__ mask, int mask_words) {
+                                                            const uint32_t* __restrict__ mask, int mask_words,
+                                                            const uint32_t* __restrict__ gate) {
+  // gate (the two-pass scan's fallback for f32 stores, k_screen.hip): run only when the screen asked for it
+  if (gate && *gate == 0u) return;
   constexpr int NKS = D / 16;   // 16-dim k-steps per tile
   constexpr int NST = D / kSK;  // stages per tile
   constexpr int KPS = kSK / 16;  // k-steps per stage (4)
@@ -270,11 +273,11 @@ __global__ __launch_bounds__(256, 1) void scan_mfma9_kernel(const float* __restr
   }
 }
 
-#define RFX_K9_ARGS X, Qp, nq, ntiles, ranges, groups, paired, tau, cs, cr, n_lists, mask, mask_words
+#define RFX_K9_ARGS X, Qp, nq, ntiles, ranges, groups, paired, tau, cs, cr, n_lists, mask, mask_words, gate
 #define RFX_K9_INSTANTIATE(DV, NAME)                                                                      \
   int NAME(int kl, dim3 grid, hipStream_t st, const float* X, const float* Qp, int nq, int ntiles,          \
            int ranges, int groups, int paired, uint32_t* tau, float* cs, int* cr, int64_t n_lists,        \
-           const uint32_t* mask, int mask_words) {                                                        \
+           const uint32_t* mask, int mask_words, const uint32_t* gate) {                                   \
     if (kl == 4 && mask)                                                                                \
       hipLaunchKernelGGL((scan_mfma9_kernel<4, DV, kModeMask>), grid, dim3(256), 0, st, RFX_K9_ARGS);       \
     else if (kl == 10 && mask)                                                                          \

@@ -6,7 +6,7 @@ namespace rfx {
 namespace k9 {
 int launch_f32_768(int kl, dim3 grid, hipStream_t st, const float* X, const float* Qp, int nq, int ntiles,
                    int ranges, int groups, int paired, uint32_t* tau, float* cs, int* cr, int64_t n_lists,
-                   const uint32_t* mask, int mask_words);
+                   const uint32_t* mask, int mask_words, const uint32_t* gate);
 }  // namespace k9
 
 size_t tau_bytes_mfma9(const MfmaPlan& p) { return (size_t)p.nq_pad * k9::kTauW * sizeof(uint32_t); }
@@ -35,14 +35,16 @@ MfmaPlan plan_scan_mfma9(int64_t nrows, int D, int dtype, int64_t nq, int k) {
 }
 
 int launch_scan_mfma9(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask) {
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask, const uint32_t* gate,
+                      bool tau_zeroed) {
+  static_assert(k9::kTauW == kFallbackTauW, "screen_queries_kernel zeroes this table for the gated fallback");
   if (!p.ok || D != 768 || dtype != RFX_F32) return -1;
   const int ntiles = (nrows + k9::kTM - 1) / k9::kTM;
-  if (hipMemsetAsync(tau, 0, tau_bytes_mfma9(p), st) != hipSuccess) return -2;
+  if (!tau_zeroed && hipMemsetAsync(tau, 0, tau_bytes_mfma9(p), st) != hipSuccess) return -2;
   const int paired = p.blocks % 8 == 0 ? 1 : 0;
   dim3 grid(p.blocks * p.q_blocks);
   return k9::launch_f32_768(p.k_lane, grid, st, (const float*)X, (const float*)Qpad, nq, ntiles, p.blocks,
-                            p.q_blocks, paired, tau, cs, cr, p.n_lists, mask, (nrows + 31) / 32);
+                            p.q_blocks, paired, tau, cs, cr, p.n_lists, mask, (nrows + 31) / 32, gate);
 }
 
 }  // namespace rfx

@@ -45,6 +45,7 @@ constexpr int kWaves = 8;
 constexpr int kTM = 32;                   // rows per tile
 constexpr int kQW = 32;                   // queries per wave
 constexpr int kQG = kWaves * kQW;         // 256 queries per workgroup
+constexpr int kQGSmall = 2 * kQW;         // the 2-wave kernel's 64 (batches of <= 64 questions)
 constexpr int kSK = 256;                  // codes (bytes) per row per stage
 constexpr int kRowB = kSK;                // 256 B per row per stage
 constexpr int kSlot = kTM * kRowB;        // 8 KB: 32 rows × 256 codes
@@ -66,19 +67,26 @@ __device__ unsigned long long g_k10_bt[1024][2];
 // trips they make (max over the wave's lanes of the passing values), summed over all waves
 __device__ unsigned int g_k10_trips[2][64];
 #endif
+// NW: waves per workgroup (kWaves = 8: 256 queries, config 3's batches; 2: 64 queries, the micro-batches of
+// 9..64 questions, two workgroups per CU).  A workgroup's slot table is NW * 32 queries x 16 slots.
+template <int NW>
+constexpr int tau_bytes_nw() { return NW * kQW * kTauW * 4; }
 template <int RING>
 constexpr int meta_off() { return RING * kSlot; }
 template <int RING>
 constexpr int tau_off() { return meta_off<RING>() + kMR * 1024; }
-template <int RING>
-constexpr int list_off() { return tau_off<RING>() + kTauBytes; }
+template <int RING, int NW = kWaves>
+constexpr int list_off() { return tau_off<RING>() + tau_bytes_nw<NW>(); }
 // per-slot arrival counters of the barrier-free ring (debug MODE 32768): ready[16], done[16], in the
 // first 128 B of the debug MODE 1024 list area (never both; both are zeroed before the first barrier)
-template <int KL, int RING>
-constexpr int ctr_off() { return list_off<RING>(); }
-template <int KL, int RING>
-constexpr int lds_bytes() { return list_off<RING>() + kWaves * KL * 64 * 8; }
+template <int KL, int RING, int NW = kWaves>
+constexpr int ctr_off() { return list_off<RING, NW>(); }
+// the list area (debug MODE 1024's LDS lists) exists in the 8-wave kernel; the 2-wave kernel keeps only the
+// 128 B of counters, so two workgroups fit a CU's LDS
+template <int KL, int RING, int NW = kWaves>
+constexpr int lds_bytes() { return list_off<RING, NW>() + (NW == kWaves ? kWaves * KL * 64 * 8 : 128); }
 static_assert(lds_bytes<10, 12>() <= 163840, "LDS budget");
+static_assert(2 * lds_bytes<16, 8, 2>() <= 163840, "two 2-wave workgroups per CU");
 
 // spin (s_sleep) until the LDS counter reaches target; bounded, so a counting error can never hang the
 // GPU (the result would be wrong, and the tests would say so)
@@ -467,8 +475,8 @@ constexpr int kModeTileBarrier = 2097152;  // one wait + barrier per tile (TB be
 constexpr int kModeFloatMask = 4194304;  // the slow path's float pass mask (fold_mask) instead of fold_mask_int
 constexpr int kModePubOnChange = 8388608;  // publish a list's best only when it rose (production; variant encoding 10^8 RING + MODE)
 constexpr int kModeSortMerge = 16384;  // a wave with >= 8 passes in some lane folds by one sorted merge (debug)
-template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0>
-__global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
+template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0, int NW = kWaves>
+__global__ __launch_bounds__(64 * NW, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
                                                              const int8_t* __restrict__ Qc, const float* __restrict__ qe2,
                                                              int nq, int ntiles, uint32_t* __restrict__ tau,
@@ -480,17 +488,23 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   constexpr int NST = D / kSK;   // stages per tile
   constexpr int KPS = kSK / 64;  // k-steps per stage (4)
   static_assert(D % kSK == 0, "D must be a multiple of 256");
-  static_assert(KL <= 10, "threshold table holds 10 slots");
-  __shared__ __attribute__((aligned(1024))) uint8_t lds[lds_bytes<KL, RING>()];
+  static_assert(KL <= 16, "the bound is the KL-th largest of 16 slots");
+  static_assert(NW == 8 || NW == 2, "8 waves (256 queries) or 2 waves (64 queries) per workgroup");
+  constexpr int NT = 64 * NW;          // threads
+  constexpr int QG = NW * kQW;         // queries per workgroup
+  constexpr int GPW = 8 / NW;          // LDS-DMA pieces per wave per stage (8 KB / 1 KB / NW)
+  constexpr int TAUB = tau_bytes_nw<NW>();
+  static_assert(TAUB / 1024 / NW == kTauGPW, "slot-table DMA pieces per wave");
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[lds_bytes<KL, RING, NW>()];
   constexpr int kTauOff = tau_off<RING>();
   constexpr int kMetaOff = meta_off<RING>();
-  constexpr int kListOff = list_off<RING>();
+  constexpr int kListOff = list_off<RING, NW>();
 
   const int tid = threadIdx.x;
   const int w = tid >> 6, lane = tid & 63;
   const int half = lane >> 5;
   const int range = blockIdx.x;
-  const int qg = blockIdx.y * kQG;
+  const int qg = blockIdx.y * QG;
   const int q = qg + w * kQW + 16 * ((lane >> 4) & 1) + (lane & 15);  // after the pair swap
   const int nblk = gridDim.x;
   // The tiles of this block: tb0 + i * tstride, i < nt.  Static split: tiles range, range + nblk, ...
@@ -535,12 +549,13 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   {
     uint4* tz = (uint4*)(lds + kTauOff);
 #pragma unroll
-    for (int i = 0; i < kTauBytes / 16 / 512; ++i) tz[tid + 512 * i] = uint4{0u, 0u, 0u, 0u};
+    for (int i = 0; i < TAUB / 16 / NT; ++i) tz[tid + NT * i] = uint4{0u, 0u, 0u, 0u};
   }
   uint64_t* const Ls = (uint64_t*)(lds + kListOff) + (w * KL) * 64 + lane;  // debug MODE 1024's list
+  if constexpr (NW == kWaves)
 #pragma unroll
-  for (int i = 0; i < KL; ++i) Ls[i * 64] = 0ull;
-  uint32_t* const ready = (uint32_t*)(lds + ctr_off<KL, RING>());  // MODE 32768: [RING] pieces landed
+    for (int i = 0; i < KL; ++i) Ls[i * 64] = 0ull;
+  uint32_t* const ready = (uint32_t*)(lds + ctr_off<KL, RING, NW>());  // MODE 32768: [RING] pieces landed
   uint32_t* const done = ready + 16;                                  // [RING] waves done reading
   if (tid < 32) ready[tid] = 0u;  // (the same zeros as the list init above)
   constexpr bool F2 = (MODE & kModeFold2) != 0 && (MODE & 1024) == 0;  // the round-5 fold (debug)
@@ -567,10 +582,15 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
     for (int ks = 0; ks < NKS; ++ks) bq[2 * ks + qb] = *(const uint4*)(qa + 64 * ks);
   }
 
-  // LDS-DMA piece of wave w: slot bytes [1024 w, +1024) = rows 4w .. 4w+3 (256 B each); lane ->
-  // (row 4w + (lane >> 4), position lane & 15) <- source chunk position ^ (row & 15)
-  const int pr = 4 * w + (lane >> 4);
-  const uint32_t laneoff = (uint32_t)(pr * D + (((lane & 15) ^ (pr & 15)) * 16));
+  // LDS-DMA piece p of a stage: slot bytes [1024 p, +1024) = rows 4p .. 4p+3 (256 B each); lane ->
+  // (row 4p + (lane >> 4), position lane & 15) <- source chunk position ^ (row & 15).  Wave w issues pieces
+  // w + NW u, u < GPW (one piece per wave in the 8-wave kernel, four in the 2-wave kernel).
+  uint32_t laneoff[GPW];
+#pragma unroll
+  for (int u = 0; u < GPW; ++u) {
+    const int pr = 4 * (w + NW * u) + (lane >> 4);
+    laneoff[u] = (uint32_t)(pr * D + (((lane & 15) ^ (pr & 15)) * 16));
+  }
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)lds;
   // The tile metadata (scale, live word) rides the same counted stream: with the piece of a tile's
   // first stage, every wave also DMAs the tile's 16-B record (64 lane copies, identical bytes from
@@ -582,8 +602,13 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
     const int ti = gi / NST;
     const int si = gi - ti * NST;
     const int8_t* tbase = X + (int64_t)tile_of(ti) * kTM * D + si * kSK;
-    const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)(slot * kSlot) + (uint32_t)(w * 1024));
-    bdma_nt(make_rsrc(tbase), laneoff, dst);  // codes are read once per batch
+    const v4i32 rs = make_rsrc(tbase);
+#pragma unroll
+    for (int u = 0; u < GPW; ++u) {
+      const uint32_t dst =
+          __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)(slot * kSlot) + (uint32_t)((w + NW * u) * 1024));
+      bdma_nt(rs, laneoff[u], dst);  // codes are read once per batch
+    }
     if (first) {
       const uint32_t mdst = __builtin_amdgcn_readfirstlane(lds_base + kMetaOff + (uint32_t)((ti % kMR) * 1024));
       bdma(meta_rsrc, (uint32_t)tile_of(ti) * 16u, mdst);
@@ -593,9 +618,9 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   auto issue_tau = [&]() {
 #pragma unroll
     for (int u = 0; u < kTauGPW; ++u) {
-      const int i = w + kWaves * u;
+      const int i = w + NW * u;
       const uint32_t dst = __builtin_amdgcn_readfirstlane(lds_base + kTauOff + i * 1024);
-      bdma_sc1(tau_rsrc, (uint32_t)(qg * kTauW * 4 + tid * 16 + u * kWaves * 1024), dst);
+      bdma_sc1(tau_rsrc, (uint32_t)(qg * kTauW * 4 + tid * 16 + u * NW * 1024), dst);
     }
   };
 
@@ -619,14 +644,18 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   // multiplication by s_t >= 0 is monotone, so the max passes whenever any value would.  Against
   // the store-wide smax bound it skips the tiles whose scale lies below smax (measured: 17 % of
   // wave-tiles entered the slow path with the smax bound).
-  float tf_own = -__builtin_inff(), tf_oth = -__builtin_inff();
   const bool odd = ((lane >> 4) & 1) != 0;
+  // a padded query (q >= nq: code 0, every A = 0) never enters the slow path: its bound is +inf and its
+  // live bits are cleared (otherwise every one of its A = 0 values would reach bound - e2 = 0 - 0 forever)
+  const bool qlive = q < nq;
+  float tf_own = qlive ? -__builtin_inff() : __builtin_inff();
+  float tf_oth = (odd ? q - 16 : q + 16) < nq ? -__builtin_inff() : __builtin_inff();  // the partner lane's query
   auto set_bounds = [&]() {
     if constexpr ((MODE & 64) != 0) {
       ti_own = ibound(thr);
       ti_oth = __shfl_xor(ti_own, 16);
     } else {
-      tf_own = thr ? unord(thr) - e2 : -__builtin_inff();
+      tf_own = !qlive ? __builtin_inff() : thr ? unord(thr) - e2 : -__builtin_inff();
       if constexpr ((MODE & kModePermBounds) != 0) {
         // the partner lane's (lane ^ 16) bound by one v_permlane16_swap: no ds_bpermute round trip
         const uint32_t b = __float_as_uint(tf_own);
@@ -680,7 +709,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   constexpr int TBD = TB ? ((RING - NST + NST - 1) / NST > 2 ? (RING - NST + NST - 1) / NST : 2) : 2;
   constexpr int RA = AHEAD + 1;           // the counted-wait arithmetic below is in stages in flight
   static_assert(AHEAD >= 3, "at least three stages in flight");
-  constexpr int YNG = (RA - 2) * kGPW;  // ops younger than the next stage
+  constexpr int YNG = (RA - 2) * GPW;  // ops younger than the next stage
   static_assert((NST * KPS) % NF == 0, "fragment rotation must realign every tile");
 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // resident queries landed before the counted stream
@@ -691,7 +720,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
   if constexpr (TB) {
     // tile 0 landed: younger are the pieces of stages NST .. AHEAD - 1 and their tile records
     constexpr int NMT = (AHEAD - 1) / NST;  // records of stages NST, 2 NST, ... <= AHEAD - 1
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((AHEAD - NST) * kGPW + NMT) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((AHEAD - NST) * GPW + NMT) : "memory");
   } else {
     // stage 0 landed: younger are stages 1 .. AHEAD - 1 and the metadata records issued with stages
     // 0 .. AHEAD - 1 (with piece 0's own record after it)
@@ -740,7 +769,7 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
           if (lane == 0) atomicAdd(tau + (int64_t)(qg + w * kQW) * kTauW + 15, 1u);
         const uint2 md = *(const uint2*)(lds + kMetaOff + (it % kMR) * 1024 + lane * 16);
         const float st = __uint_as_float(md.x);
-        uint32_t lw = md.y;
+        uint32_t lw = qlive ? md.y : 0u;
         if constexpr (MASK) lw &= mask[tile];
 #pragma unroll
         for (int rb = 0; rb < 2; ++rb)
@@ -871,11 +900,11 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
             switch (nt_) {
 #define RFX_K10_TWAIT(N)                                                                                      \
   case N:                                                                                                     \
-    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"((RING - 2 * NST) * kGPW + NMY + N) : "memory");        \
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"((RING - 2 * NST) * GPW + NMY + N) : "memory");         \
     break;
               RFX_K10_TWAIT(0) RFX_K10_TWAIT(2)
               default:  // stricter, never looser
-                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"((RING - 2 * NST) * kGPW + NMY) : "memory");
+                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"((RING - 2 * NST) * GPW + NMY) : "memory");
 #undef RFX_K10_TWAIT
             }
             asm volatile("s_barrier" ::: "memory");
@@ -1016,6 +1045,35 @@ __global__ __launch_bounds__(512, 1) void scan_screen_kernel(const int8_t* __res
 // atomics): 0.3344 against 0.3461 ms at the shard, 2.039 against 2.038 ms at 10M (profiles/r05/k10_pub_ab_*.txt).
 constexpr int kProdRing = 10;
 constexpr int kProdMode = kModeTileBarrier | kModePubOnChange;
+// The 2-wave kernel (64 queries per workgroup, two workgroups per CU): the per-tile barrier over an 8-slot ring
+// at d 768 (RING >= 2 NST + 2); at d 1024 (NST 4) the per-stage barrier over 8 slots (round 4's schedule), which
+// keeps two workgroups within a CU's LDS
+template <int D>
+constexpr int w2_ring() { return 8; }
+template <int D>
+constexpr int w2_mode() { return D == 768 ? kProdMode : kModePubOnChange; }
+#define RFX_K10_INSTANTIATE_W2(DV, NAME)                                                                      \
+  int NAME(int kl, dim3 grid, hipStream_t st, const int8_t* X, const uint4* tm, const uint32_t* sts,           \
+           const int8_t* Qc, const float* qe2, int nq, int ntiles, uint32_t* tau, float* cs, int* cr,          \
+           uint32_t* dr, int64_t n_lists, const uint32_t* mask, uint32_t* xb, uint32_t* xw) {               \
+    constexpr int R = w2_ring<DV>(), M = w2_mode<DV>();                                                     \
+    if (kl == 4 && !mask)                                                                                   \
+      hipLaunchKernelGGL((scan_screen_kernel<4, DV, false, R, M, 2>), grid, dim3(128), 0, st, X, tm, sts, Qc,  \
+                         qe2, nq, ntiles, tau, cs, cr, dr, n_lists, mask, xb, xw);                           \
+    else if (kl == 10 && !mask)                                                                             \
+      hipLaunchKernelGGL((scan_screen_kernel<10, DV, false, R, M, 2>), grid, dim3(128), 0, st, X, tm, sts, Qc, \
+                         qe2, nq, ntiles, tau, cs, cr, dr, n_lists, mask, xb, xw);                           \
+    else if (kl == 4)                                                                                       \
+      hipLaunchKernelGGL((scan_screen_kernel<4, DV, true, R, M, 2>), grid, dim3(128), 0, st, X, tm, sts, Qc,   \
+                         qe2, nq, ntiles, tau, cs, cr, dr, n_lists, mask, xb, xw);                           \
+    else if (kl == 10)                                                                                      \
+      hipLaunchKernelGGL((scan_screen_kernel<10, DV, true, R, M, 2>), grid, dim3(128), 0, st, X, tm, sts, Qc,  \
+                         qe2, nq, ntiles, tau, cs, cr, dr, n_lists, mask, xb, xw);                           \
+    else                                                                                                    \
+      return -1;                                                                                            \
+    return 0;                                                                                               \
+  }
+
 // one translation unit per D instantiates the kernel for KL in {4, 10}, with and without a filter mask
 #define RFX_K10_INSTANTIATE(DV, NAME)                                                                         \
   int NAME(int kl, dim3 grid, hipStream_t st, const int8_t* X, const uint4* tm, const uint32_t* sts,           \

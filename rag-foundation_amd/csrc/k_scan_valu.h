@@ -143,6 +143,9 @@ __device__ __forceinline__ void rescore_final(const Rescore& rs, int64_t q, int 
                     : (long long)__hip_atomic_load((const unsigned long long*)out_r + o, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT);
     }
+    // an entry whose row lies outside this index's [row_offset, row_offset + rows) is padding (ADVICE r5:
+    // rfx_rescore_topk takes hand-assembled answers; a merged multi-shard row must not index past X)
+    if (row < row_offset || row - row_offset >= rs.rows) row = -1;
     double acc = 0.0;
     if (row >= 0) {
       const int64_t xr = (row - row_offset) * rs.D, qr = q * rs.D;
@@ -160,15 +163,28 @@ __device__ __forceinline__ void rescore_final(const Rescore& rs, int64_t q, int 
   if (tid < k_out) {
     const float s = rs_s[tid];
     const long long r = rs_r[tid];
+    int n_valid = 0;
+    for (int f = 0; f < k_out; ++f) n_valid += rs_r[f] >= 0;
     if (r >= 0) {
+      // rank among the valid entries (a repeated entry ranks after its earlier copy: every rank is taken once)
       int rank = 0;
-      for (int f = 0; f < k_out; ++f) rank += rs_r[f] >= 0 && better64(rs_s[f], rs_r[f], s, r);
+      for (int f = 0; f < k_out; ++f)
+        rank += rs_r[f] >= 0 && (better64(rs_s[f], rs_r[f], s, r) || (f < tid && rs_s[f] == s && rs_r[f] == r));
       const int64_t o = q * k_out + rank;
       if (out_rec) {
         out_rec[o] = MergeRec{s, 0, r};
       } else {
         out_s[o] = s;
         out_r[o] = r;
+      }
+    }
+    if (tid >= n_valid) {  // the padding goes last, whatever positions it held
+      const int64_t o = q * k_out + tid;
+      if (out_rec) {
+        out_rec[o] = MergeRec{-__builtin_inff(), 0, -1};
+      } else {
+        out_s[o] = -__builtin_inff();
+        out_r[o] = -1;
       }
     }
   }
@@ -436,14 +452,14 @@ __device__ __forceinline__ void scan_valu_body(const uint8_t* __restrict__ X, in
         __syncthreads();
         merge_one<K, false, 4, true>(lsrc, q0 + qi, K, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
         __syncthreads();
-        rescore_final(Rescore{X, Qf, D, DT}, q0 + qi, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
+        rescore_final(Rescore{X, Qf, D, DT, (int64_t)nrows}, q0 + qi, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
       }
     } else {
       const AgentSrc src{cand_s, cand_r, n};
       for (int qi = 0; qi < nqt; ++qi) {
         merge_one<K, false, 4, true>(src, q0 + qi, K, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
         __syncthreads();
-        rescore_final(Rescore{X, Qf, D, DT}, q0 + qi, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
+        rescore_final(Rescore{X, Qf, D, DT, (int64_t)nrows}, q0 + qi, fo.k_out, 0, fo.out_s, fo.out_r, nullptr);
       }
     }
     if (tid < nqt && tau) tau[q0 + tid] = 0u;  // every block's bound updates precede its arrival

@@ -16,6 +16,8 @@ namespace k10 {
            uint32_t* dr, int64_t n_lists, const uint32_t* mask, uint32_t* xb, uint32_t* xw);
 RFX_K10_DECL(launch_768)
 RFX_K10_DECL(launch_1024)
+RFX_K10_DECL(launch_768_w2)
+RFX_K10_DECL(launch_1024_w2)
 #undef RFX_K10_DECL
 }  // namespace k10
 
@@ -164,11 +166,12 @@ __global__ __launch_bounds__(256) void screen_quantize_kernel(const void* __rest
 __device__ uint32_t g_xcd_w[24];
 
 template <int DT, int D>
-__global__ __launch_bounds__(256) void screen_queries_kernel(const uint16_t* __restrict__ Q, int nq, int nq_pad,
+__global__ __launch_bounds__(256) void screen_queries_kernel(const void* __restrict__ Q, int nq, int nq_pad,
                                                              int8_t* __restrict__ Qc, float* __restrict__ qe2,
                                                              const uint32_t* __restrict__ stats,
                                                              uint32_t* __restrict__ tau, uint32_t* __restrict__ gate,
-                                                             uint32_t* __restrict__ ftau, uint32_t* __restrict__ xb) {
+                                                             uint32_t* __restrict__ ftau, int ftau_nq,
+                                                             uint32_t* __restrict__ xb) {
   constexpr int NM = D / 256;
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -204,21 +207,31 @@ __global__ __launch_bounds__(256) void screen_queries_kernel(const uint16_t* __r
       xb[x] = w;
     }
   }
+  // the gated fallback's threshold table, over ITS padded batch (kernel 6 / 8 / 9 pad to 256 / 128 / 128
+  // queries, which can exceed this launch's nq_pad: the grid covers both)
+  if (ftau && q < ftau_nq && lane < kFallbackTauW) ftau[(int64_t)q * kFallbackTauW + lane] = 0u;
   if (q >= nq_pad) return;
   if (lane < k10::kTauW) tau[(int64_t)q * k10::kTauW + lane] = 0u;
-  if (ftau && lane < kFallbackTauW) ftau[(int64_t)q * kFallbackTauW + lane] = 0u;  // the gated fallback's table
   float y[NM][4];
   float am = 0.f;
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
-    uint2 v = uint2{0u, 0u};
-    if (q < nq) v = *(const uint2*)(Q + (int64_t)q * D + 256 * m + 4 * lane);
-    const uint32_t u[2] = {v.x, v.y};
+    if constexpr (DT == RFX_F32) {
+      float4 v = float4{0.f, 0.f, 0.f, 0.f};
+      if (q < nq) v = *(const float4*)((const float*)Q + (int64_t)q * D + 256 * m + 4 * lane);
+      y[m][0] = v.x;
+      y[m][1] = v.y;
+      y[m][2] = v.z;
+      y[m][3] = v.w;
+    } else {
+      uint2 v = uint2{0u, 0u};
+      if (q < nq) v = *(const uint2*)((const uint16_t*)Q + (int64_t)q * D + 256 * m + 4 * lane);
+      const uint32_t u[2] = {v.x, v.y};
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      y[m][e] = widen<DT>((uint16_t)(e & 1 ? u[e >> 1] >> 16 : u[e >> 1] & 0xffffu));
-      am = fmaxf(am, fabsf(y[m][e]));
+      for (int e = 0; e < 4; ++e) y[m][e] = widen<DT>((uint16_t)(e & 1 ? u[e >> 1] >> 16 : u[e >> 1] & 0xffffu));
     }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) am = fmaxf(am, fabsf(y[m][e]));
   }
   am = wave_max_f32(am);  // DPP + readlane, no ds_bpermute round trips (rfx_device.h)
   const float s = am > 0.f ? __fdiv_rn(am, 127.f) : 0.f;
@@ -265,12 +278,31 @@ __device__ unsigned long long g_sel_t[256][8];
 #define RFX_SEL_T(i)
 #endif
 
+// one 16-B chunk's products added to acc in f64 (f32 products of bf16 / f16 values are exact; f32 values are
+// multiplied in f64, also exact)
+template <int DT>
+__device__ __forceinline__ void chunk_dot(double& acc, const uint4& x, const uint4& y) {
+  const uint32_t xx[4] = {x.x, x.y, x.z, x.w};
+  const uint32_t yy[4] = {y.x, y.y, y.z, y.w};
+  if constexpr (DT == RFX_F32) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc += (double)__uint_as_float(xx[e]) * (double)__uint_as_float(yy[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint16_t xh = (uint16_t)(e & 1 ? xx[e >> 1] >> 16 : xx[e >> 1] & 0xffffu);
+      const uint16_t yh = (uint16_t)(e & 1 ? yy[e >> 1] >> 16 : yy[e >> 1] & 0xffffu);
+      acc += (double)(widen<DT>(xh) * widen<DT>(yh));
+    }
+  }
+}
+
 template <int DT, int D>
 __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restrict__ cs, const int* __restrict__ cr,
                                                             const uint32_t* __restrict__ drops, int64_t n_lists,
                                                             int list_len, const float* __restrict__ qe2,
-                                                            const uint16_t* __restrict__ Q,
-                                                            const uint16_t* __restrict__ X, int k, int64_t row_offset,
+                                                            const uint8_t* __restrict__ Q,
+                                                            const uint8_t* __restrict__ X, int k, int64_t row_offset,
                                                             float* __restrict__ out_s, int64_t* __restrict__ out_r,
                                                             Rec* __restrict__ out_rec, uint32_t* __restrict__ gate,
                                                             int* __restrict__ diag, int force) {
@@ -279,7 +311,10 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
   // The exact re-score: 16 lanes per survivor row (CPL 16-B chunks of the row per lane), U rows per
   // 16-lane group in flight: 8 waves x 4 groups x U = 96 rows per round (config 3: 94 survivors on
   // average, so one round, one memory latency)
-  constexpr int NT = 512, NW = NT / 64, CPL = D / 128, U = 3, U1 = 10, RPR = NW * 4 * U;
+  // rows and queries are read as 16-B chunks: chunk c of a row holds its bytes [16 c, 16 c + 16) (8 bf16 / f16
+  // or 4 f32 elements); lane gl of a 16-lane group takes chunks gl + 16 i, i < CPL
+  constexpr int RB = D * (DT == RFX_F32 ? 4 : 2);
+  constexpr int NT = 512, NW = NT / 64, CPL = RB / 256, U = DT == RFX_F32 ? 2 : 3, U1 = 10, RPR = NW * 4 * U;
   __shared__ __attribute__((aligned(16))) float ca[kSelCap];  // screen score A of kept candidate i
   __shared__ int crow[kSelCap];   // its row
   __shared__ int srow[kSelCap];   // survivor j's row
@@ -300,7 +335,7 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
   const int gl = lane & 15, grp = w * 4 + (lane >> 4);
   uint4 yq[CPL];
 #pragma unroll
-  for (int c = 0; c < CPL; ++c) yq[c] = *(const uint4*)(Q + q * D + (gl + 16 * c) * 8);
+  for (int c = 0; c < CPL; ++c) yq[c] = *(const uint4*)(Q + q * RB + (gl + 16 * c) * 16);
   __syncthreads();
   // 1. compact the kept candidates (the scan wrote -inf for empty slots and dropped entries)
   const int64_t n = n_lists * list_len;
@@ -387,22 +422,13 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
       const int j = j0 + u * NW * 4;
       const int64_t row = j < ns ? (int64_t)srow[j] : (int64_t)srow[0];
 #pragma unroll
-      for (int c = 0; c < CPL; ++c) xv[u][c] = *(const uint4*)(X + row * D + (gl + 16 * c) * 8);
+      for (int c = 0; c < CPL; ++c) xv[u][c] = *(const uint4*)(X + row * RB + (gl + 16 * c) * 16);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       double acc = 0.0;
 #pragma unroll
-      for (int c = 0; c < CPL; ++c) {
-        const uint32_t xx[4] = {xv[u][c].x, xv[u][c].y, xv[u][c].z, xv[u][c].w};
-        const uint32_t yy[4] = {yq[c].x, yq[c].y, yq[c].z, yq[c].w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const uint16_t xh = (uint16_t)(e & 1 ? xx[e >> 1] >> 16 : xx[e >> 1] & 0xffffu);
-          const uint16_t yh = (uint16_t)(e & 1 ? yy[e >> 1] >> 16 : yy[e >> 1] & 0xffffu);
-          acc += (double)(widen<DT>(xh) * widen<DT>(yh));
-        }
-      }
+      for (int c = 0; c < CPL; ++c) chunk_dot<DT>(acc, xv[u][c], yq[c]);
       acc = row16_sum_f64(acc);  // within the 16-lane group (DPP; lane 0's sum = the xor butterfly's)
       const int j = j0 + u * NW * 4;
       if (gl == 0 && j < ns) skey[j] = ((uint64_t)ord((float)acc) << 32) | (uint32_t)(~(uint32_t)srow[j]);
@@ -477,18 +503,38 @@ void launch_screen_quantize(const void* X, int D, int dtype, int64_t tile0, int6
 #undef RFX_SQ
 }
 
+// Batches of up to 64 questions (the micro-batches of rfx/batcher.py: <= 50 chat threads per process,
+// config.py:137, chat.py:496-521) run the 2-wave kernel: 64 queries per workgroup, two workgroups per CU,
+// 512 workgroups over the corpus (fewer on a small store: >= 8 tiles each).  Larger batches the 8-wave
+// kernel (256 queries per workgroup, one per CU).  RFX_SCREEN_W2_BLOCKS (tuning) overrides the former's count.
+int screen_w2_blocks() {
+  static const int v = [] {
+    const char* e = getenv("RFX_SCREEN_W2_BLOCKS");
+    return e && *e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k, int max_blocks) {
   MfmaPlan p{};
   p.ok = screen_supported(D, dtype) && nrows > 0;
   p.k_lane = k <= 4 ? 4 : (k <= 10 ? 10 : -1);
   if (p.k_lane < 0) p.ok = false;
-  p.bn = k10::kQG;
-  p.q_blocks = (int)((nq + k10::kQG - 1) / k10::kQG);
-  p.nq_pad = (int64_t)p.q_blocks * k10::kQG;
+  const bool w2 = nq <= k10::kQGSmall;
+  p.bn = w2 ? k10::kQGSmall : k10::kQG;
+  p.q_blocks = (int)((nq + p.bn - 1) / p.bn);
+  p.nq_pad = (int64_t)p.q_blocks * p.bn;
   if (p.q_blocks < 1 || p.q_blocks > 256) p.ok = false;
   const int64_t ntiles = std::max<int64_t>((nrows + k10::kTM - 1) / k10::kTM, 1);
-  int64_t ranges = std::max<int64_t>((max_blocks > 0 ? max_blocks : 256) / std::max(p.q_blocks, 1), 1);
-  ranges = std::min<int64_t>(ranges, ntiles);
+  int64_t ranges;
+  if (w2) {
+    ranges = max_blocks > 0 ? max_blocks : screen_w2_blocks() > 0 ? screen_w2_blocks() : 512;
+    ranges = std::min<int64_t>(ranges, std::max<int64_t>(ntiles / 8, 8));
+    if (ranges > 8) ranges = ranges / 8 * 8;  // (a multiple of 8: the XCD-balanced split)
+  } else {
+    ranges = std::max<int64_t>((max_blocks > 0 ? max_blocks : 256) / std::max(p.q_blocks, 1), 1);
+  }
+  ranges = std::max<int64_t>(std::min<int64_t>(ranges, ntiles), 1);
   p.blocks = (int)ranges;
   p.tiles_per_block = (int)((ntiles + ranges - 1) / ranges);
   p.lists_per_block = 2;
@@ -510,15 +556,21 @@ uint32_t* xcd_weights_device_ptr() {
 }
 
 void launch_screen_queries(const void* Q, int dtype, int D, int64_t nq, int64_t nq_pad, int8_t* Qc, float* qe2,
-                           const uint32_t* stats, uint32_t* tau, uint32_t* gate, uint32_t* ftau, hipStream_t st) {
-  const dim3 grid((unsigned)((nq_pad + 3) / 4));
+                           const uint32_t* stats, uint32_t* tau, uint32_t* gate, uint32_t* ftau, int64_t ftau_nq,
+                           hipStream_t st) {
+  if (!ftau) ftau_nq = 0;
+  const dim3 grid((unsigned)((std::max(nq_pad, ftau_nq) + 3) / 4));
 #define RFX_SQQ(DTV, DV)                                                                                       \
-  hipLaunchKernelGGL((screen_queries_kernel<DTV, DV>), grid, dim3(256), 0, st, (const uint16_t*)Q, (int)nq,      \
-                     (int)nq_pad, Qc, qe2, stats, tau, gate, ftau, tau + nq_pad * k10::kTauW)
+  hipLaunchKernelGGL((screen_queries_kernel<DTV, DV>), grid, dim3(256), 0, st, Q, (int)nq, (int)nq_pad, Qc, qe2,  \
+                     stats, tau, gate, ftau, (int)ftau_nq, tau + nq_pad * k10::kTauW)
   if (dtype == RFX_BF16 && D == 768)
     RFX_SQQ(RFX_BF16, 768);
   else if (dtype == RFX_BF16)
     RFX_SQQ(RFX_BF16, 1024);
+  else if (dtype == RFX_F32 && D == 768)
+    RFX_SQQ(RFX_F32, 768);
+  else if (dtype == RFX_F32)
+    RFX_SQQ(RFX_F32, 1024);
   else if (D == 768)
     RFX_SQQ(RFX_F16, 768);
   else
@@ -532,7 +584,8 @@ int launch_scan_screen(const MfmaPlan& p, const int8_t* codes, const void* tmeta
   if (!p.ok || (D != 768 && D != 1024)) return -1;
   const int ntiles = (nrows + k10::kTM - 1) / k10::kTM;
   dim3 grid(p.blocks, p.q_blocks);
-  auto f = D == 768 ? k10::launch_768 : k10::launch_1024;
+  auto f = p.bn == k10::kQGSmall ? (D == 768 ? k10::launch_768_w2 : k10::launch_1024_w2)
+                                 : (D == 768 ? k10::launch_768 : k10::launch_1024);
   return f(p.k_lane, grid, st, codes, (const uint4*)tmeta, stats, Qc, qe2, nq, ntiles, tau, cs, cr, drops, p.n_lists,
            mask, tau + p.nq_pad * k10::kTauW, xcd_weights_device_ptr());
 }
@@ -545,12 +598,16 @@ int launch_screen_select(const float* cs, const int* cr, const uint32_t* drops, 
   if (k < 1 || k > kSelK) return -1;
 #define RFX_SEL(DTV, DV)                                                                                          \
   hipLaunchKernelGGL((screen_select_kernel<DTV, DV>), dim3((unsigned)nq), dim3(512), 0, st, cs, cr, drops, n_lists, \
-                     list_len, qe2, (const uint16_t*)Q, (const uint16_t*)X, k, row_offset, out_s, out_r,           \
+                     list_len, qe2, (const uint8_t*)Q, (const uint8_t*)X, k, row_offset, out_s, out_r,             \
                      (Rec*)out_rec, gate, diag, force)
   if (dtype == RFX_BF16 && D == 768)
     RFX_SEL(RFX_BF16, 768);
   else if (dtype == RFX_BF16)
     RFX_SEL(RFX_BF16, 1024);
+  else if (dtype == RFX_F32 && D == 768)
+    RFX_SEL(RFX_F32, 768);
+  else if (dtype == RFX_F32)
+    RFX_SEL(RFX_F32, 1024);
   else if (D == 768)
     RFX_SEL(RFX_F16, 768);
   else

@@ -17,6 +17,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <thread>
 #include <cstdlib>
 #include <cerrno>
 #include <cmath>
@@ -55,6 +58,104 @@ int fail(int code, const char* fmt, ...) {
 int esize(int dtype) { return dtype == RFX_F32 ? 4 : 2; }
 bool valid_dtype(int dtype) { return dtype == RFX_F32 || dtype == RFX_BF16 || dtype == RFX_F16; }
 
+// ---- index memory: physical allocations mapped through HIP virtual memory ---------------------------------
+// An index's rows and its int8 copy each live in ONE physical allocation (hipMemCreate) mapped at a reserved
+// address range of their own.  A union view (rfx_union_create; a question over several stores,
+// gemini_rag.py:463-469) maps the members' physical allocations back to back into one more range: one
+// contiguous [rows][dim] image of all members that IS their memory (no copy; appends and tombstones show
+// through).  Sizes are multiples of the recommended granularity (capacity_align below).  Unmapping memory a
+// kernel still reads would fault the GPU: every release below follows a device synchronisation.
+struct Phys {
+  hipMemGenericAllocationHandle_t h{};
+  size_t bytes = 0;
+  ~Phys() {
+    if (bytes) (void)hipMemRelease(h);
+  }
+};
+struct Mapping {
+  void* va = nullptr;
+  size_t bytes = 0;
+  std::vector<std::shared_ptr<Phys>> parts;  // mapped back to back from va
+  ~Mapping() {
+    size_t off = 0;
+    for (auto& p : parts) {
+      (void)hipMemUnmap((uint8_t*)va + off, p->bytes);
+      off += p->bytes;
+    }
+    if (va) (void)hipMemAddressFree(va, bytes);
+  }
+};
+
+hipMemAllocationProp vmm_prop(int device) {
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = device;
+  return prop;
+}
+
+// the recommended granularity of the device, 0 when its virtual memory API is unavailable (or RFX_VMM=0:
+// plain hipMalloc, no zero-copy union views)
+size_t vmm_granularity(int device) {
+  static std::mutex mu;
+  static std::map<int, size_t> g;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = g.find(device);
+  if (it != g.end()) return it->second;
+  size_t v = 0;
+  const char* e = getenv("RFX_VMM");
+  int vmm = 0;
+  if (!(e && e[0] == '0') && hipDeviceGetAttribute(&vmm, hipDeviceAttributeVirtualMemoryManagementSupported, device) == hipSuccess &&
+      vmm) {
+    const hipMemAllocationProp prop = vmm_prop(device);
+    if (hipMemGetAllocationGranularity(&v, &prop, hipMemAllocationGranularityRecommended) != hipSuccess) v = 0;
+  }
+  g[device] = v;
+  return v;
+}
+
+// map `parts` back to back into a fresh range (read / write for the device)
+int vmm_map(int device, const std::vector<std::shared_ptr<Phys>>& parts, std::shared_ptr<Mapping>& out) {
+  auto m = std::make_shared<Mapping>();
+  for (auto& p : parts) m->bytes += p->bytes;
+  const size_t g = vmm_granularity(device);
+  if (!g || m->bytes == 0) return fail(RFX_EUNSUPPORTED, "virtual memory unavailable on device %d", device);
+  if (hipMemAddressReserve(&m->va, m->bytes, g, nullptr, 0) != hipSuccess) {
+    m->va = nullptr;
+    return fail(RFX_ENOMEM, "hipMemAddressReserve(%zu) failed", m->bytes);
+  }
+  size_t off = 0;
+  for (auto& p : parts) {
+    if (hipMemMap((uint8_t*)m->va + off, p->bytes, 0, p->h, 0) != hipSuccess)
+      return fail(RFX_ENOMEM, "hipMemMap(%zu) failed", p->bytes);  // (~Mapping unmaps what was mapped)
+    m->parts.push_back(p);
+    off += p->bytes;
+  }
+  hipMemAccessDesc acc = {};
+  acc.location = vmm_prop(device).location;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  if (hipMemSetAccess(m->va, m->bytes, &acc, 1) != hipSuccess) return fail(RFX_ENOMEM, "hipMemSetAccess failed");
+  out = m;
+  return RFX_OK;
+}
+
+// one physical allocation of `bytes` (a multiple of the granularity) at a range of its own
+int vmm_alloc(int device, size_t bytes, std::shared_ptr<Mapping>& out) {
+  auto p = std::make_shared<Phys>();
+  p->bytes = bytes;
+  const hipMemAllocationProp prop = vmm_prop(device);
+  if (hipMemCreate(&p->h, bytes, &prop, 0) != hipSuccess) {
+    p->bytes = 0;
+    std::memset(&p->h, 0, sizeof(p->h));
+    // (a failed create leaves no handle: the destructor's release of a zero handle is a no-op error)
+    return fail(RFX_ENOMEM, "hipMemCreate(%zu) failed", bytes);
+  }
+  return vmm_map(device, {p}, out);
+}
+
+int64_t gcd64(int64_t a, int64_t b) { return b ? gcd64(b, a % b) : a; }
+int64_t lcm64(int64_t a, int64_t b) { return a / gcd64(a, b) * b; }
+
 struct Index {
   int device = 0;
   int dim = 0;
@@ -63,6 +164,14 @@ struct Index {
   int64_t capacity = 0;
   int64_t live = 0;
   void* data = nullptr;
+  // the rows' and the int8 codes' mappings (virtual memory; null with plain hipMalloc buffers); a union view
+  // holds its members' physical allocations through its own mappings
+  std::shared_ptr<Mapping> rows_map, codes_map;
+  bool view = false;         // a union view (rfx_union_create): read-only, owns no physical memory of its own
+  int64_t layout_gen = 0;    // bumped whenever data / scodes move (growth, a rebuilt or dropped copy)
+  std::vector<int64_t> view_bases;                  // a view: member m's rows start at view_bases[m]
+  std::vector<std::weak_ptr<Index>> view_members;   // a view: its members
+  std::vector<int64_t> view_gens;                   // a view: the members' layout_gen at creation
   std::vector<uint8_t> tomb;  // host bitmap (1 = deleted), mirrors the NaN rows on device
   std::shared_timed_mutex mu;
   // per-stream launch state of the single-launch VALU search (zeroed once, left zero by every
@@ -83,7 +192,14 @@ struct Index {
 };
 
 void screen_free(Index& ix) {
-  for (void* p : {(void*)ix.scodes, ix.smeta, (void*)ix.sstats})
+  if (ix.codes_map || ix.scodes) ++ix.layout_gen;
+  if (ix.codes_map) {
+    (void)hipDeviceSynchronize();  // no search still reads the codes: then unmap
+    ix.codes_map.reset();
+  } else if (ix.scodes) {
+    (void)hipFree(ix.scodes);
+  }
+  for (void* p : {ix.smeta, (void*)ix.sstats})
     if (p) (void)hipFree(p);
   ix.scodes = nullptr;
   ix.smeta = nullptr;
@@ -125,8 +241,14 @@ int screen_build(Index& ix, hipStream_t st) {
   }
   screen_free(ix);
   if (cap == 0) return RFX_OK;
-  if (hipMalloc(&ix.scodes, (size_t)cap * ix.dim) != hipSuccess || hipMalloc(&ix.smeta, (size_t)nt * 16) != hipSuccess ||
-      hipMalloc(&ix.sstats, 256) != hipSuccess) {
+  bool codes_ok;
+  if (ix.rows_map) {  // the codes in virtual memory too (capacity_align: cap * dim is a whole number of granules)
+    codes_ok = vmm_alloc(ix.device, (size_t)cap * ix.dim, ix.codes_map) == RFX_OK;
+    ix.scodes = codes_ok ? (int8_t*)ix.codes_map->va : nullptr;
+  } else {
+    codes_ok = hipMalloc(&ix.scodes, (size_t)cap * ix.dim) == hipSuccess;
+  }
+  if (!codes_ok || hipMalloc(&ix.smeta, (size_t)nt * 16) != hipSuccess || hipMalloc(&ix.sstats, 256) != hipSuccess) {
     screen_free(ix);
     return fail(RFX_ECAPACITY, "hipMalloc failed for the int8 screen copy (%lld rows)", (long long)cap);
   }
@@ -214,7 +336,8 @@ std::chrono::milliseconds lock_timeout() {
 }
 #define RFX_WLOCK(ix)                                                                            \
   std::unique_lock<std::shared_timed_mutex> lk((ix)->mu, std::defer_lock);                        \
-  if (!lk.try_lock_for(lock_timeout())) return fail(RFX_EBUSY, "index busy: writer lock timed out")
+  if (!lk.try_lock_for(lock_timeout())) return fail(RFX_EBUSY, "index busy: writer lock timed out"); \
+  if ((ix)->view) return fail(RFX_EINVAL, "a union view is read-only (write to its member stores)")
 #define RFX_RLOCK(ix)                                                                            \
   std::shared_lock<std::shared_timed_mutex> lk((ix)->mu, std::defer_lock);                        \
   if (!lk.try_lock_for(lock_timeout())) return fail(RFX_EBUSY, "index busy: reader lock timed out")
@@ -241,21 +364,45 @@ int fill_tail_nan(Index& ix, hipStream_t st) {
   return RFX_OK;
 }
 
+// Capacity granule (rows): whole 128-row scan tiles; with virtual memory also a whole number of granules of
+// the rows' bytes AND of the int8 copy's (d bytes per row), so members of a union view map back to back at
+// row bases that are multiples of 128 (8,192 rows at d 768 with a 2-MiB granule).
+int64_t capacity_align(const Index& ix) {
+  const int64_t g = (int64_t)vmm_granularity(ix.device);
+  if (!g) return 128;
+  return lcm64(lcm64(128, g / gcd64(g, ix.row_bytes())), g / gcd64(g, (int64_t)ix.dim));
+}
+
 int grow(Index& ix, int64_t need, hipStream_t st) {
   if (need <= ix.capacity) return RFX_OK;
   int64_t cap = ix.capacity > 0 ? ix.capacity : 1024;
   while (cap < need) cap = cap + cap / 2 + 1024;
-  cap = (cap + 127) / 128 * 128;  // whole 128-row scan tiles
+  const int64_t al = capacity_align(ix);
+  cap = (cap + al - 1) / al * al;
   void* p = nullptr;
+  std::shared_ptr<Mapping> m;
   const size_t bytes = (size_t)cap * ix.row_bytes();
-  if (hipMalloc(&p, bytes) != hipSuccess) return fail(RFX_ENOMEM, "hipMalloc(%zu) failed for index", bytes);
+  if (vmm_granularity(ix.device)) {
+    const int rc = vmm_alloc(ix.device, bytes, m);
+    if (rc) return fail(RFX_ENOMEM, "device memory for %lld rows: %s", (long long)cap, g_err.c_str());
+    p = m->va;
+  } else if (hipMalloc(&p, bytes) != hipSuccess) {
+    return fail(RFX_ENOMEM, "hipMalloc(%zu) failed for index", bytes);
+  }
   if (ix.rows > 0) {
     RFX_HIP(hipMemcpyAsync(p, ix.data, (size_t)ix.rows * ix.row_bytes(), hipMemcpyDeviceToDevice, st));
     RFX_HIP(hipStreamSynchronize(st));
   }
-  if (ix.data) RFX_HIP(hipFree(ix.data));  // hipFree waits for in-flight work on the old buffer
+  if (ix.rows_map) {
+    RFX_HIP(hipDeviceSynchronize());  // no search still reads the old rows: then unmap
+    ix.rows_map.reset();
+  } else if (ix.data) {
+    RFX_HIP(hipFree(ix.data));  // hipFree waits for in-flight work on the old buffer
+  }
+  ix.rows_map = m;
   ix.data = p;
   ix.capacity = cap;
+  ++ix.layout_gen;
   return fill_tail_nan(ix, st);
 }
 
@@ -297,39 +444,26 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L, bool search
   L = SearchLayout{};
   L.vp = rfx::plan_scan_valu(ix.rows, ix.dim, ix.dtype, nq, k);
   L.kernel = 0;
+  // With an int8 copy every batch of nq > 8 (k <= 10) takes the two-pass scan (kernel 10: the 8-wave kernel
+  // for nq > 64, the 2-wave one for 9..64), whose gated fallback is the exact scan planned here: kernel 6
+  // (bf16 / f16, d 768), 8 (d 1024) or 9 (f32, d 768) whatever nq, padded to their query groups.
+  const bool two_pass = search && ix.screen && ix.rows > 0 && k <= 10 && rfx::screen_supported(ix.dim, ix.dtype);
   if (nq > 8) {
-    // (with an int8 copy, 64 < nq <= 128 also plans kernel 6: it is the two-pass scan's fallback)
-    if (nq > 128 || (search && ix.screen && nq > 64)) {
+    if (nq > 128 || (two_pass && nq > 8)) {
       L.mp = rfx::plan_scan_mfma6(ix.rows, ix.dim, ix.dtype, nq, k);
       if (L.mp.ok) L.kernel = 6;
     }
-    if (L.kernel == 0 && nq > 64) {
-      // d = 1024: kernel 8 (k-split wave pairs); the debug build's RFX_D1024_KERNEL=7 selects its
-      // predecessor kernel 7 (16 queries per wave) for A/B runs
-#ifdef RFX_DEBUG_BUILD
-      static const int d1024 = [] {
-        const char* e = getenv("RFX_D1024_KERNEL");
-        return e && *e ? atoi(e) : 8;
-      }();
-#else
-      constexpr int d1024 = 8;
-#endif
-      if (d1024 == 7) {
-#ifdef RFX_DEBUG_BUILD
-        L.mp = rfx::plan_scan_mfma7(ix.rows, ix.dim, ix.dtype, nq, k);
-        if (L.mp.ok) L.kernel = 7;
-#endif
-      } else {
-        L.mp = rfx::plan_scan_mfma8(ix.rows, ix.dim, ix.dtype, nq, k);
-        if (L.mp.ok) L.kernel = 8;
-      }
+    if (L.kernel == 0 && (nq > 64 || two_pass)) {  // d = 1024: kernel 8 (k-split wave pairs)
+      L.mp = rfx::plan_scan_mfma8(ix.rows, ix.dim, ix.dtype, nq, k);
+      if (L.mp.ok) L.kernel = 8;
     }
     if (L.kernel == 0 && nq > 64) {
       L.mp = rfx::plan_scan_mfma3(ix.rows, ix.dim, ix.dtype, nq, k);
       if (L.mp.ok) L.kernel = 3;
     }
     if (L.kernel == 0 && ix.dtype == RFX_F32) {
-      L.mp = rfx::plan_scan_mfma9(ix.rows, ix.dim, ix.dtype, nq, k);
+      // (kernel 9 plans nq > 16; as the two-pass scan's fallback it also takes 9..16 questions, padded to 128)
+      L.mp = rfx::plan_scan_mfma9(ix.rows, ix.dim, ix.dtype, two_pass ? std::max<int64_t>(nq, 17) : nq, k);
       if (L.mp.ok) L.kernel = 9;
     }
     if (L.kernel == 0 && nq > 128) {
@@ -347,10 +481,6 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L, bool search
     L.q_bytes = (size_t)L.mp.nq_pad * ix.dim * (L.kernel == 9 ? 4 : 2);
     if (L.kernel == 6)  // (the debug build's kernel-5 ablations use the same [nq_pad][16] table)
       tau_bytes = rfx::tau_bytes_mfma6(L.mp);
-#ifdef RFX_DEBUG_BUILD
-    else if (L.kernel == 7)
-      tau_bytes = rfx::tau_bytes_mfma7(L.mp);
-#endif
     else if (L.kernel == 8)
       tau_bytes = rfx::tau_bytes_mfma8(L.mp);
     else if (L.kernel == 9)
@@ -370,7 +500,7 @@ int make_layout(const Index& ix, int64_t nq, int k, SearchLayout& L, bool search
   L.cr_off = L.cs_off + align_up((size_t)nq * L.n_cand * 4);
   L.total = L.cr_off + align_up((size_t)nq * L.n_cand * 4);
   L.fbk = 0;
-  if (search && ix.screen && ix.rows > 0 && (L.kernel == 6 || L.kernel == 8)) {
+  if (search && ix.screen && ix.rows > 0 && (L.kernel == 6 || L.kernel == 8 || L.kernel == 9)) {
     L.sp = rfx::plan_scan_screen(ix.rows, ix.dim, ix.dtype, nq, k, scan_blocks);
     // the regions are sized (and placed) by the default plan, the most workgroups and lists any
     // scan_blocks gives: every offset, the gate and diag words included, is then the same whatever
@@ -477,9 +607,6 @@ int scan_into(Index& ix, const SearchLayout& L, const void* queries, int64_t nq,
     uint32_t* tau = (uint32_t*)(ws + L.tau_off);
     const int rc =
         L.kernel == 6 ? rfx::launch_scan_mfma6(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
-#ifdef RFX_DEBUG_BUILD
-        : L.kernel == 7 ? rfx::launch_scan_mfma7(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
-#endif
         : L.kernel == 8 ? rfx::launch_scan_mfma8(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
         : L.kernel == 9 ? rfx::launch_scan_mfma9(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
         : L.kernel == 3 ? rfx::launch_scan_mfma3(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs, cr, st, mask)
@@ -514,12 +641,10 @@ int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t
   uint32_t* gate = (uint32_t*)(ws + L.s_gate);
   int* diag = (int*)(ws + L.s_diag);
   uint32_t* tau = (uint32_t*)(ws + L.tau_off);
-  // the fallback's threshold table is zeroed by the query quantiser when it covers the fallback's
-  // padded batch (kernel 10 pads to 256 queries, kernels 6 / 8 to 256 / 128): no memset launch
-  const bool ftau = L.mp.nq_pad <= L.sp.nq_pad;
+  // the fallback's threshold table ([its nq_pad][16]) is zeroed by the query quantiser: no memset launch
   if (stages & 1) {
-    rfx::launch_screen_queries(queries, ix.dtype, ix.dim, nq, L.sp.nq_pad, qc, qe2, ix.sstats, stau, gate,
-                               ftau ? tau : nullptr, st);
+    rfx::launch_screen_queries(queries, ix.dtype, ix.dim, nq, L.sp.nq_pad, qc, qe2, ix.sstats, stau, gate, tau,
+                               L.mp.nq_pad, st);
     if (ev0) RFX_HIP(hipEventRecord((hipEvent_t)ev0, st));
     if (rfx::launch_scan_screen(L.sp, ix.scodes, ix.smeta, ix.sstats, (int)ix.rows, ix.dim, qc, qe2, (int)nq, stau, scs,
                                 scr, drops, st, mask) != 0)
@@ -535,7 +660,7 @@ int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t
   const void* qpad = queries;
   if (nq != L.mp.nq_pad || ((uintptr_t)queries & 15)) {
     qpad = ws + L.q_off;
-    rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, 2, (void*)qpad, st);
+    rfx::launch_pad_queries(queries, nq, L.mp.nq_pad, ix.dim, esize(ix.dtype), (void*)qpad, st);
   }
   if (rfx::launch_screen_select(scs, scr, drops, L.sp.n_lists, L.sp.k_lane, qe2, qpad, ix.data, ix.dim, ix.dtype, nq,
                                 k, row_offset, out_s, out_r, out_rec, gate, diag, ix.screen == 2, st) != 0)
@@ -544,12 +669,14 @@ int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t
   float* cs = (float*)(ws + L.cs_off);
   int32_t* cr = (int32_t*)(ws + L.cr_off);
   const int rc = L.fbk == 6 ? rfx::launch_scan_mfma6(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs,
-                                                     cr, st, mask, gate, ftau)
-                            : rfx::launch_scan_mfma8(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs,
-                                                     cr, st, mask, gate, ftau);
+                                                     cr, st, mask, gate, true)
+                 : L.fbk == 8 ? rfx::launch_scan_mfma8(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs,
+                                                       cr, st, mask, gate, true)
+                              : rfx::launch_scan_mfma9(L.mp, ix.data, (int)ix.rows, ix.dim, ix.dtype, qpad, (int)nq, tau, cs,
+                                                       cr, st, mask, gate, true);
   if (rc != 0) return fail(RFX_EUNSUPPORTED, "fallback scan launch rejected (%d)", rc);
   // (the fallback's final top-k re-scored by the two-pass rule: the same bits as the select's answer)
-  const rfx::Rescore rs{ix.data, queries, ix.dim, ix.dtype};
+  const rfx::Rescore rs{ix.data, queries, ix.dim, ix.dtype, ix.rows};
   if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.n_cand, L.mp.k_lane, k, row_offset, out_rec ? nullptr : out_s,
                                    out_rec ? nullptr : out_r, out_rec, st, /*sorted=*/true, gate, &rs) != 0)
     return fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
@@ -671,7 +798,11 @@ int rfx_index_destroy(rfx_index_t h) {
   }
   std::unique_lock<std::shared_timed_mutex> lk(ix->mu);  // waits for in-flight searches: never EBUSY
   RFX_HIP(hipSetDevice(ix->device));
-  if (ix->data) {
+  if (ix->rows_map || ix->view) {
+    RFX_HIP(hipDeviceSynchronize());  // no launch still reads the mapped rows: then unmap
+    ix->rows_map.reset();
+    ix->data = nullptr;
+  } else if (ix->data) {
     RFX_HIP(hipFree(ix->data));
     ix->data = nullptr;
   }
@@ -679,6 +810,131 @@ int rfx_index_destroy(rfx_index_t h) {
   ix->fused_state.clear();
   screen_free(*ix);
   return RFX_OK;
+}
+
+// ---- union views (a question over several stores in one launch; gemini_rag.py:463-469) ------------------------
+}  // extern "C"
+namespace {
+__global__ void stats_max_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst) {
+  if (threadIdx.x < 3) atomicMax(dst + threadIdx.x, src[threadIdx.x]);  // non-negative f32 bits order as u32
+}
+
+// the members of a view, locked shared for the caller's scope; `stale` when one is gone or moved its memory
+struct ViewMembers {
+  std::vector<std::shared_ptr<Index>> ix;
+  std::vector<std::shared_lock<std::shared_timed_mutex>> locks;
+  bool stale = false;
+};
+int lock_members(const Index& v, ViewMembers& vm) {
+  for (size_t m = 0; m < v.view_members.size(); ++m) {
+    auto ix = v.view_members[m].lock();
+    if (!ix) {
+      vm.stale = true;
+      return RFX_OK;
+    }
+    std::shared_lock<std::shared_timed_mutex> lk(ix->mu, std::defer_lock);
+    if (!lk.try_lock_for(lock_timeout())) return fail(RFX_EBUSY, "union member busy: reader lock timed out");
+    if (ix->layout_gen != v.view_gens[m] || (v.screen != 0) != (ix->screen != 0 && ix->scodes != nullptr)) vm.stale = true;
+    vm.ix.push_back(ix);
+    vm.locks.push_back(std::move(lk));
+  }
+  return RFX_OK;
+}
+
+// the view's own bytes: the members' tile records copied into one table and the max of their stats
+int view_refresh(Index& v, const ViewMembers& vm, hipStream_t st) {
+  if (!v.screen) return RFX_OK;
+  RFX_HIP(hipMemsetAsync(v.sstats, 0, 256, st));
+  for (size_t m = 0; m < vm.ix.size(); ++m) {
+    const Index& ix = *vm.ix[m];
+    RFX_HIP(hipMemcpyAsync((uint8_t*)v.smeta + v.view_bases[m] / 32 * 16, ix.smeta, (size_t)ix.capacity / 32 * 16,
+                           hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(stats_max_kernel, dim3(1), dim3(64), 0, st, ix.sstats, v.sstats);
+  }
+  RFX_HIP(hipGetLastError());
+  return RFX_OK;
+}
+}  // namespace
+extern "C" {
+
+int rfx_union_create(const rfx_index_t* members, int n, void* stream, rfx_index_t* out, int64_t* out_bases) {
+  if (!members || n < 1 || !out) return fail(RFX_EINVAL, "null members / out, or n < 1");
+  auto v = std::make_shared<Index>();
+  v->view = true;
+  ViewMembers vm;
+  for (int m = 0; m < n; ++m) {
+    auto ix = get(members[m]);
+    if (!ix) return fail(RFX_EINVAL, "unknown index handle (member %d)", m);
+    if (ix->view) return fail(RFX_EINVAL, "member %d is itself a union view", m);
+    if (m == 0) {
+      v->device = ix->device;
+      v->dim = ix->dim;
+      v->dtype = ix->dtype;
+    } else if (ix->device != v->device || ix->dim != v->dim || ix->dtype != v->dtype) {
+      return fail(RFX_EINVAL, "member %d differs in device / dim / dtype", m);
+    }
+    v->view_members.push_back(ix);
+  }
+  RFX_HIP(hipSetDevice(v->device));
+  if (!vmm_granularity(v->device)) return fail(RFX_EUNSUPPORTED, "union views need HIP virtual memory (RFX_VMM=0?)");
+  v->view_gens.assign((size_t)n, 0);
+  for (int m = 0; m < n; ++m) v->view_gens[m] = v->view_members[m].lock()->layout_gen;
+  int rc = lock_members(*v, vm);
+  if (rc) return rc;
+  if ((int)vm.ix.size() != n) return fail(RFX_EINVAL, "a member was destroyed meanwhile");
+  bool screened = true;
+  std::vector<std::shared_ptr<Phys>> rows_parts, code_parts;
+  for (int m = 0; m < n; ++m) {
+    const Index& ix = *vm.ix[m];
+    if (!ix.rows_map || ix.capacity == 0)
+      return fail(RFX_EUNSUPPORTED, "member %d has no mapped rows (empty, or made without virtual memory)", m);
+    v->view_bases.push_back(v->capacity);
+    v->capacity += ix.capacity;
+    v->live += ix.live;
+    rows_parts.insert(rows_parts.end(), ix.rows_map->parts.begin(), ix.rows_map->parts.end());
+    screened = screened && ix.screen && ix.codes_map && ix.scap == ix.capacity;
+    if (screened) code_parts.insert(code_parts.end(), ix.codes_map->parts.begin(), ix.codes_map->parts.end());
+  }
+  if ((rc = vmm_map(v->device, rows_parts, v->rows_map))) return rc;
+  v->data = v->rows_map->va;
+  v->rows = v->capacity;
+  v->tomb.assign((size_t)(v->rows + 7) / 8, 0);
+  if (screened) {
+    if ((rc = vmm_map(v->device, code_parts, v->codes_map))) return rc;
+    v->scodes = (int8_t*)v->codes_map->va;
+    v->scap = v->capacity;
+    if (hipMalloc(&v->smeta, (size_t)v->capacity / 32 * 16) != hipSuccess || hipMalloc(&v->sstats, 256) != hipSuccess) {
+      screen_free(*v);
+      return fail(RFX_ENOMEM, "hipMalloc failed for the view's tile records");
+    }
+    v->screen = 1;
+    if ((rc = view_refresh(*v, vm, (hipStream_t)stream))) return rc;
+  }
+  for (auto& ix : vm.ix)
+    if (ix->screen_dropped) v->screen_dropped = 1;
+  if (out_bases)
+    for (int m = 0; m < n; ++m) out_bases[m] = v->view_bases[m];
+  const uint64_t h = g_next++;
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_reg[h] = v;
+  }
+  *out = h;
+  return RFX_OK;
+}
+
+int rfx_union_refresh(rfx_index_t view, void* stream, int* out_stale) {
+  auto v = get(view);
+  if (!v || !out_stale) return fail(RFX_EINVAL, "unknown view handle / null out");
+  if (!v->view) return fail(RFX_EINVAL, "not a union view");
+  std::unique_lock<std::shared_timed_mutex> lk(v->mu, std::defer_lock);  // (searches of the view read the records)
+  if (!lk.try_lock_for(lock_timeout())) return fail(RFX_EBUSY, "view busy: lock timed out");
+  RFX_HIP(hipSetDevice(v->device));
+  ViewMembers vm;
+  int rc = lock_members(*v, vm);
+  if (rc) return rc;
+  *out_stale = vm.stale ? 1 : 0;
+  return vm.stale ? RFX_OK : view_refresh(*v, vm, (hipStream_t)stream);
 }
 
 int rfx_index_info(rfx_index_t h, int* dim, int* dtype, int64_t* rows, int64_t* capacity, int64_t* live_rows) {
@@ -1127,7 +1383,7 @@ int rfx_rescore_topk(rfx_index_t h, const void* queries_d, int64_t nq, int k, in
     return fail(RFX_EINVAL, "null queries / answer");
   RFX_RLOCK(ix);
   RFX_HIP(hipSetDevice(ix->device));
-  const rfx::Rescore rs{ix->data, queries_d, ix->dim, ix->dtype};
+  const rfx::Rescore rs{ix->data, queries_d, ix->dim, ix->dtype, ix->rows};
   rfx::launch_rescore_topk(rs, nq, k, row_offset, records_d ? nullptr : scores_d, records_d ? nullptr : rows_d,
                            records_d, (hipStream_t)stream);
   RFX_HIP(hipGetLastError());
@@ -1195,12 +1451,6 @@ int rfx_dbg_scan_variant(rfx_index_t h, const void* queries_d, int64_t nq, int k
   if (mode >= 20000000)  // headline kernel (k_scan_mfma6.h) ablations: mode 20000000 + MODE
     rc2 = rfx::launch_scan_mfma6_dbg(rfx::plan_scan_mfma6(ix->rows, ix->dim, ix->dtype, nq, k), mode - 20000000, ix->data,
                                      (int)ix->rows, ix->dtype, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st);
-  else if (mode >= 1000 && mode < 16000000)  // kernel-5 ablations: mode 1000 + MODE
-    rc2 = rfx::launch_scan_mfma5_dbg(rfx::plan_scan_mfma5(ix->rows, ix->dim, ix->dtype, nq, k), mode - 1000, ix->data,
-                                     (int)ix->rows, ix->dtype, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st);
-  else if (mode >= 20 && mode < 1000)  // all-query-stationary kernel ablations: mode 20 + MODE
-    rc2 = rfx::launch_scan_mfma4_dbg(rfx::plan_scan_mfma4(ix->rows, ix->dim, ix->dtype, nq, k), mode - 20, ix->data,
-                                     (int)ix->rows, ix->dtype, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off), cs, cr, st);
   else if (mode >= 10 && mode < 20)  // 256x256 kernel ablations: mode 10 + MODE
     rc2 = rfx::launch_scan_mfma2_dbg(rfx::plan_scan_mfma2(ix->rows, ix->dim, ix->dtype, nq, k), mode - 10, ix->data,
                                      (int)ix->rows, ix->dim, qpad, (int)nq, (uint32_t*)((uint8_t*)ws_d + L.tau_off),
@@ -1249,7 +1499,7 @@ int rfx_dbg_screen_variant(rfx_index_t h, const void* queries_d, int64_t nq, int
   float* qe2 = (float*)(ws + L.s_qe2);
   uint32_t* stau = (uint32_t*)(ws + L.s_tau);
   rfx::launch_screen_queries(queries_d, ix->dtype, ix->dim, nq, L.sp.nq_pad, qc, qe2, ix->sstats, stau,
-                             (uint32_t*)(ws + L.s_gate), nullptr, st);
+                             (uint32_t*)(ws + L.s_gate), nullptr, 0, st);
   // RFX_DBG_KEEP_TAU=1: the slot table starts from the previous launch's final one (the same queries on
   // the same rows: still a lower bound of a_k) — the timing of a bound with no warm-up at all
   static const bool keep_tau = getenv("RFX_DBG_KEEP_TAU") != nullptr;
@@ -1290,7 +1540,7 @@ int rfx_dbg_screen_search(rfx_index_t h, const void* queries_d, int64_t nq, int 
   float* qe2 = (float*)(ws + L.s_qe2);
   uint32_t* stau = (uint32_t*)(ws + L.s_tau);
   uint32_t* gate = (uint32_t*)(ws + L.s_gate);
-  rfx::launch_screen_queries(queries_d, ix->dtype, ix->dim, nq, L.sp.nq_pad, qc, qe2, ix->sstats, stau, gate, nullptr, st);
+  rfx::launch_screen_queries(queries_d, ix->dtype, ix->dim, nq, L.sp.nq_pad, qc, qe2, ix->sstats, stau, gate, nullptr, 0, st);
   if (rfx::launch_scan_screen_dbg(L.sp, variant, ix->scodes, ix->smeta, ix->sstats, (int)ix->rows, qc, qe2, (int)nq, stau,
                                   (float*)(ws + L.s_cs), (int*)(ws + L.s_cr), (uint32_t*)(ws + L.s_drop), st) != 0)
     return fail(RFX_EUNSUPPORTED, "screen variant %d unsupported", variant);
@@ -1495,7 +1745,7 @@ int search_impl(rfx_index_t h, const void* queries_d, int64_t nq, int k, const u
   }
   // the scan's candidates are sorted lists: the merge bounds admission by the lists' k-th entries; its
   // final top-k is re-scored by the score rule of every plan (fl32 of the f64 dot; k_scan_valu.h)
-  const rfx::Rescore rs{ix->data, queries_d, ix->dim, ix->dtype};
+  const rfx::Rescore rs{ix->data, queries_d, ix->dim, ix->dtype, ix->rows};
   if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, n_cand, list_len, k, row_offset, out_rec ? nullptr : out_scores_d,
                                    out_rec ? nullptr : out_rows_d, out_rec, st, /*sorted=*/n_cand > 0, nullptr,
                                    n_cand > 0 ? &rs : nullptr) != 0)
@@ -1523,7 +1773,65 @@ int rfx_search_records(rfx_index_t h, const void* queries_d, int64_t nq, int k, 
 }
 
 // ---- one search over a row-sharded store, issued from C++ -----------------------------------
+}  // extern "C"
 namespace {
+// The shards' launch sequences are issued by a pool of host threads, one task per shard (one
+// thread issuing 8 shards x ~6 launches took ~0.24 ms, ~0.7x of a real 8-GPU step).  The caller's thread
+// waits for the ISSUE of every task (not for the GPU), then enqueues the exchange and the merge.  Workers are
+// made on first use (at most kIssueThreads) and live for the process; RFX_ISSUE_THREADS=0 keeps the serial
+// issue (A/B runs).
+constexpr int kIssueThreads = 16;
+struct IssuePool {
+  std::mutex mu;
+  std::condition_variable cv, done_cv;
+  std::vector<std::thread> workers;
+  std::vector<std::function<void()>> tasks;  // this round's tasks; workers take them by index
+  size_t next = 0, done = 0;
+  uint64_t round = 0;
+  std::mutex call_mu;  // one round at a time
+  void ensure(size_t n) {
+    while (workers.size() < std::min<size_t>(n, kIssueThreads)) {
+      workers.emplace_back([this] {
+        uint64_t seen = 0;
+        for (;;) {
+          std::function<void()> f;
+          {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return round != seen && next < tasks.size(); });
+            f = tasks[next++];
+            if (next == tasks.size()) seen = round;
+          }
+          f();
+          std::lock_guard<std::mutex> lk(mu);
+          if (++done == tasks.size()) done_cv.notify_all();
+        }
+      });
+      workers.back().detach();
+    }
+  }
+  void run(std::vector<std::function<void()>>& fs) {
+    std::lock_guard<std::mutex> call(call_mu);
+    ensure(fs.size());
+    std::unique_lock<std::mutex> lk(mu);
+    tasks.swap(fs);
+    next = done = 0;
+    ++round;
+    cv.notify_all();
+    done_cv.wait(lk, [&] { return done == tasks.size(); });
+    tasks.clear();
+  }
+};
+IssuePool& issue_pool() {
+  static IssuePool* p = new IssuePool();  // (never destroyed: detached workers outlive static destruction)
+  return *p;
+}
+bool parallel_issue() {
+  static const bool on = [] {
+    const char* e = getenv("RFX_ISSUE_THREADS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 // events for the cross-stream orderings of rfx_sharded_search: per thread and device, reused call after
 // call (a stream that waited on an event keeps the state it saw when the wait was enqueued)
 hipEvent_t pooled_event(int device, int slot) {
@@ -1537,6 +1845,7 @@ hipEvent_t pooled_event(int device, int slot) {
   return v[slot];
 }
 }  // namespace
+extern "C" {
 
 int rfx_sharded_search(int n, const rfx_index_t* handles, const int64_t* bases, const void* queries_d,
                        void* const* qbuf_d, int64_t nq, int k, const uint32_t* const* masks_d,
@@ -1556,6 +1865,13 @@ int rfx_sharded_search(int n, const rfx_index_t* handles, const int64_t* bases, 
     dev[i] = ix->device;
     if (i == 0) qbytes = nq * ix->row_bytes();
     if (!comm && dev[i] != dev[0]) return fail(RFX_EINVAL, "shards on several devices need a communicator");
+    // every shard's workspace is checked before anything is enqueued: a regrow-and-retry by the
+    // caller then never follows the partial work of the shards before a failing one
+    RFX_RLOCK(ix);
+    SearchLayout L;
+    if (int rc = make_search_layout(*ix, nq, k, L)) return rc;
+    if (ws_bytes[i] < L.total || (L.total && !ws_d[i]))
+      return fail(RFX_EINVAL, "workspace too small (%zu < %zu, shard %d)", ws_bytes[i], L.total, i);
   }
   const size_t rec_bytes = (size_t)nq * k * 16;
   hipStream_t src = (hipStream_t)src_stream;
@@ -1579,19 +1895,33 @@ int rfx_sharded_search(int n, const rfx_index_t* handles, const int64_t* bases, 
   }
   // 2. per shard: the queries on its device (a peer copy when it has a buffer there), then its whole search
   // (rfx_search_records: the two-pass scan where the shard holds its int8 copy) into [nq][k] records with its
-  // base added
-  for (int i = 0; i < n; ++i) {
+  // base added — one issue task per shard, run by the pool's threads side by side
+  std::vector<int> rcs((size_t)n, RFX_OK);
+  std::vector<std::string> errs((size_t)n);
+  auto shard_issue = [&](int i) {
     hipStream_t st = (hipStream_t)streams[i];
-    RFX_HIP(hipSetDevice(dev[i]));
+    int rc = hipSetDevice(dev[i]) == hipSuccess ? RFX_OK : fail(RFX_EDEVICE, "hipSetDevice(%d) failed", dev[i]);
     const void* q = queries_d;
-    if (qbuf_d && qbuf_d[i] && qbuf_d[i] != queries_d) {
-      RFX_HIP(hipMemcpyAsync(qbuf_d[i], queries_d, (size_t)qbytes, hipMemcpyDeviceToDevice, st));
+    if (!rc && qbuf_d && qbuf_d[i] && qbuf_d[i] != queries_d) {
+      if (hipMemcpyAsync(qbuf_d[i], queries_d, (size_t)qbytes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        rc = fail(RFX_EDEVICE, "query copy to shard %d failed", i);
       q = qbuf_d[i];
     }
-    const int rc = search_impl(handles[i], q, nq, k, masks_d ? masks_d[i] : nullptr, mask_words ? mask_words[i] : 0,
-                               bases[i], nullptr, nullptr, recs_d[i], ws_d[i], ws_bytes[i], st, nullptr, nullptr);
-    if (rc) return rc;
+    if (!rc)
+      rc = search_impl(handles[i], q, nq, k, masks_d ? masks_d[i] : nullptr, mask_words ? mask_words[i] : 0, bases[i],
+                       nullptr, nullptr, recs_d[i], ws_d[i], ws_bytes[i], st, nullptr, nullptr);
+    rcs[i] = rc;
+    if (rc) errs[i] = g_err;  // (thread-local: carried back to the caller's thread)
+  };
+  if (parallel_issue() && n > 1) {
+    std::vector<std::function<void()>> fs;
+    for (int i = 0; i < n; ++i) fs.push_back([&shard_issue, i] { shard_issue(i); });
+    issue_pool().run(fs);
+  } else {
+    for (int i = 0; i < n; ++i) shard_issue(i);
   }
+  for (int i = 0; i < n; ++i)
+    if (rcs[i]) return fail(rcs[i], "shard %d: %s", i, errs[i].c_str());
   // 3. the exchange: one RCCL gather to shard 0's device over distinct devices; shards sharing one device
   // stack their records there (in place when recs_d[i] already is row i of gathered_d), ordered by events
   if (comm) {

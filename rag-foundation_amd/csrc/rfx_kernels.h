@@ -13,6 +13,7 @@ struct Rescore {
   const void* Q = nullptr;  // the queries [nq][D] in the index dtype
   int D = 0;
   int dtype = 0;
+  int64_t rows = 0;  // rows of X: an entry's row outside [row_offset, row_offset + rows) is padding
 };
 
 // ---- generator / maintenance -------------------------------------------------------------
@@ -94,18 +95,6 @@ int launch_scan_mfma2_dbg(const MfmaPlan& p, int mode, const void* X, int nrows,
 MfmaPlan plan_scan_mfma3(int64_t nrows, int D, int dtype, int64_t nq, int k);
 int launch_scan_mfma3(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
                       uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
-size_t tau_bytes_mfma4(const MfmaPlan& p);
-MfmaPlan plan_scan_mfma4(int64_t nrows, int D, int dtype, int64_t nq, int k);
-int launch_scan_mfma4(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st);
-int launch_scan_mfma4_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, int dtype, const void* Qpad, int nq,
-                          uint32_t* tau, float* cs, int* cr, hipStream_t st);
-size_t tau_bytes_mfma5(const MfmaPlan& p);
-MfmaPlan plan_scan_mfma5(int64_t nrows, int D, int dtype, int64_t nq, int k);
-int launch_scan_mfma5(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
-int launch_scan_mfma5_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, int dtype, const void* Qpad, int nq,
-                          uint32_t* tau, float* cs, int* cr, hipStream_t st);
 size_t tau_bytes_mfma6(const MfmaPlan& p);
 MfmaPlan plan_scan_mfma6(int64_t nrows, int D, int dtype, int64_t nq, int k);
 // gate (optional): a device word; the launch does nothing unless it is non-zero (the exact pass of
@@ -115,10 +104,6 @@ int launch_scan_mfma6(const MfmaPlan& p, const void* X, int nrows, int D, int dt
                       const uint32_t* gate = nullptr, bool tau_zeroed = false);
 int launch_scan_mfma6_dbg(const MfmaPlan& p, int mode, const void* X, int nrows, int dtype, const void* Qpad, int nq,
                           uint32_t* tau, float* cs, int* cr, hipStream_t st);
-size_t tau_bytes_mfma7(const MfmaPlan& p);
-MfmaPlan plan_scan_mfma7(int64_t nrows, int D, int dtype, int64_t nq, int k);
-int launch_scan_mfma7(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
 size_t tau_bytes_mfma8(const MfmaPlan& p);
 MfmaPlan plan_scan_mfma8(int64_t nrows, int D, int dtype, int64_t nq, int k);
 int launch_scan_mfma8(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
@@ -127,8 +112,10 @@ int launch_scan_mfma8(const MfmaPlan& p, const void* X, int nrows, int D, int dt
 // f32 stores (kernel 9): batched scan on v_mfma_f32_16x16x4_f32 for 16 < nq
 size_t tau_bytes_mfma9(const MfmaPlan& p);
 MfmaPlan plan_scan_mfma9(int64_t nrows, int D, int dtype, int64_t nq, int k);
+// gate / tau_zeroed: as kernel 6 (the exact pass of the two-pass scan of an f32 store)
 int launch_scan_mfma9(const MfmaPlan& p, const void* X, int nrows, int D, int dtype, const void* Qpad, int nq,
-                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr);
+                      uint32_t* tau, float* cs, int* cr, hipStream_t st, const uint32_t* mask = nullptr,
+                      const uint32_t* gate = nullptr, bool tau_zeroed = false);
 void launch_pad_queries(const void* Q, int64_t nq, int64_t nq_pad, int D, int esz, void* out,
                         hipStream_t st);
 
@@ -160,8 +147,10 @@ uint32_t* xcd_weights_device_ptr();  // kernel 10's per-device XCD weight table 
 // ftau (or null): the gated fallback scan's threshold table ([nq_pad][kFallbackTauW], kernel 6 / 8),
 // zeroed here so the fallback launch needs no memset of its own (tau_zeroed below)
 constexpr int kFallbackTauW = 16;
+// ftau_nq: the fallback's padded batch (its table rows zeroed; may exceed nq_pad)
 void launch_screen_queries(const void* Q, int dtype, int D, int64_t nq, int64_t nq_pad, int8_t* Qc, float* qe2,
-                           const uint32_t* stats, uint32_t* tau, uint32_t* gate, uint32_t* ftau, hipStream_t st);
+                           const uint32_t* stats, uint32_t* tau, uint32_t* gate, uint32_t* ftau, int64_t ftau_nq,
+                           hipStream_t st);
 int launch_scan_screen(const MfmaPlan& p, const int8_t* codes, const void* tmeta, const uint32_t* stats, int nrows, int D,
                        const int8_t* Qc, const float* qe2, int nq, uint32_t* tau, float* cs, int* cr, uint32_t* drops,
                        hipStream_t st, const uint32_t* mask);

@@ -101,6 +101,8 @@ SIGNATURES = {
     "rfx_index_create": ([_i, _i, _i, _i64, _pu64], _i),
     "rfx_index_destroy": ([_u64], _i),
     "rfx_index_info": ([_u64, _pi, _pi, _pi64, _pi64, _pi64], _i),
+    "rfx_union_create": ([_pu64, _i, _p, _pu64, _pi64], _i),
+    "rfx_union_refresh": ([_u64, _p, _pi], _i),
     "rfx_index_reserve": ([_u64, _i64], _i),
     "rfx_index_add": ([_u64, _p, _i64, _i, _pi64, _p], _i),
     "rfx_index_add_synthetic": ([_u64, _u64, _i64, _i64, _pi64, _p], _i),

@@ -85,6 +85,11 @@ class DeviceIndex:
         return self._info()[0]
 
     @property
+    def capacity(self) -> int:
+        """Rows the device buffer holds (rows beyond `rows` are NaN); a union view maps members whole."""
+        return self._info()[1]
+
+    @property
     def live_rows(self) -> int:
         return self._info()[2]
 

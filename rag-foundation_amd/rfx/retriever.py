@@ -234,8 +234,14 @@ class GpuRetriever:
         if need > budget:
             return None
         with _STATE_LOCK:  # room for it (bytes reserved while it is built)
-            while _UNIONS and _UNION_BYTES[0] + need > budget:
+            # an evicted view stays counted until _close_unions uncounts it (after the lock), so the loop
+            # keeps its own tally of what the evictions free: only the least recently used views that make
+            # room go.  A pinned view frees nothing until its last user releases it.
+            freed = 0
+            while _UNIONS and _UNION_BYTES[0] - freed + need > budget:
+                n0 = len(closing)
                 _evict_union(next(iter(_UNIONS)), closing)
+                freed += sum(v.nbytes for v in closing[n0:])
             _UNION_BYTES[0] += need
             if self.registry.on_evict.count(_purge_batchers) == 0:
                 self.registry.on_evict.append(_purge_batchers)

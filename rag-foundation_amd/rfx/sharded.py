@@ -261,8 +261,12 @@ class ShardedIndex:
             rec_n_a = max(b["rec_n"], rec_n) if keep else rec_n
             q_n_a = max(b["q_n"], nq * self.dim) if keep else nq * self.dim
             nq_a, k_a = (max(b["nq"], nq), max(b["k"], k)) if keep else (nq, k)
-            ws = [torch.empty(sh.workspace_bytes(nq_a, k_a) * 5 // 4 + 4096, dtype=torch.uint8,
-                              device=torch.device("cuda", d)) for sh, d in zip(self.shards, self.devices)]
+            # the workspace a plan needs is not monotone in nq or k (kernel 11's region exists for nq <= 8 only,
+            # the VALU and MFMA plans size their lists differently): room for the largest batch seen AND for this
+            # one
+            ws = [torch.empty(max(sh.workspace_bytes(nq_a, k_a), sh.workspace_bytes(nq, k)) * 5 // 4 + 4096,
+                              dtype=torch.uint8, device=torch.device("cuda", d))
+                  for sh, d in zip(self.shards, self.devices)]
             dev0 = torch.device("cuda", self.devices[0])
             gathered = torch.empty(n * rec_n_a, dtype=torch.int64, device=dev0)
             recs = None if shared else [torch.empty(rec_n_a, dtype=torch.int64, device=torch.device("cuda", d))
@@ -282,7 +286,9 @@ class ShardedIndex:
         """One rfx_sharded_search call: every shard's search, the exchange and the merge enqueued from C++
         (VERDICT r4 #5: the per-shard Python path issued each shard's copy, search and exchange itself)."""
         n, nq = len(self.shards), queries.shape[0]
-        q = queries.contiguous()
+        # the C side reads nq rows of the index dtype and dim from this pointer: the same checks as the
+        # per-shard path's search_records (ADVICE r5), so a wrong dtype or dim raises instead of reading garbage
+        q = self.shards[0]._check_queries(queries)
         if q.device.index != self.devices[0]:
             q = q.to(torch.device("cuda", self.devices[0]))
         src = torch.cuda.current_stream(q.device)

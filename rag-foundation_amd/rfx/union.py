@@ -2,6 +2,17 @@
 stores (the file-search tool's `file_search_store_names`, gemini_rag.py:463-469) is ONE scan launch
 and one merge instead of one per store plus a host merge.
 
+Zero copy (round 6, the default): rfx_union_create maps the members' device memory (their rows, and their
+int8 copies when every member holds one) back to back into one address range through HIP virtual memory, so
+the view IS the members' memory.  Member i owns the view rows [base_i, base_i + capacity_i): its rows, then
+its NaN tail.  Appends within a member's capacity and tombstones show through at once; `follow` only copies
+the members' tile records again (16 B per 32 rows, the view's own bytes with 256 B of stats) and rebuilds
+the view — a new mapping, still no copy — when a member moved its memory (growth past its capacity, a
+rebuilt or dropped int8 copy).  RFX_UNION_COPY=1 (or a device without virtual memory) keeps the copying
+view below.
+
+The copying view:
+
 Layout: store i owns the union row range [base_i, base_i + region_i); its rows [0, rows_i) sit at
 [base_i, base_i + rows_i), the rest of the region is NaN headroom (never returned, like a
 tombstone).  Bases and regions are multiples of 32 (a row-mask word never straddles two stores).
@@ -20,16 +31,21 @@ Eligible: every member a flat DeviceIndex store (IVF stores answer from their li
 from their shards) on one device with one dim / dtype, and RFX_UNION_MAX_ROWS (default 16M) union
 rows; the retriever's view cache is bounded in bytes (RFX_UNION_MAX_BYTES, LRU; rfx.retriever).
 """
+import ctypes
 import os
 
 import numpy as np
 import torch
 
 from . import filters
-from ._lib import ESIZE
+from ._lib import ESIZE, RFX_EUNSUPPORTED, check, lib
 from .index import DeviceIndex
 
 ALIGN = 32
+
+
+def zero_copy() -> bool:
+    return os.environ.get("RFX_UNION_COPY", "0") != "1"
 
 
 def union_key(stores):
@@ -42,6 +58,8 @@ def _region(rows: int) -> int:
 
 
 def planned_rows(stores) -> int:
+    if zero_copy():
+        return sum(max(st.index.capacity, 1) for st in stores)
     return sum(_region(st.index.rows) for st in stores)
 
 
@@ -53,10 +71,13 @@ def members_screened(stores) -> bool:
 
 
 def planned_bytes(stores) -> int:
-    """Device bytes a view over `stores` would hold: the rows, and the int8 copy when the members
-    answer with the two-pass scan (dim bytes per row)."""
+    """Device bytes a view over `stores` would hold of its own: zero copy, the tile records of the int8 copy
+    (16 B per 32 rows) and its stats when the members answer with the two-pass scan; copying, the rows and
+    the int8 copy (dim bytes per row)."""
     st0 = stores[0]
     n = planned_rows(stores)
+    if zero_copy():
+        return (n // ALIGN * 16 + 256) if members_screened(stores) else 0
     return n * st0.dim * (ESIZE[st0.dtype] + (1 if members_screened(stores) else 0))
 
 
@@ -84,6 +105,35 @@ class UnionView:
         self.bases, self.rows, self.regions, self.tombs = [], [], [], []
         self.rows_copied = 0  # rows this view copied from its members (tests / profiles: O(appended))
         self.users, self.evicted = 0, False  # pins of the retriever's view cache (rfx.retriever)
+        self.mapped = zero_copy() and self._map(stores)
+        if not self.mapped:
+            self._build_copy(stores)
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(torch.device("cuda", self.device)).cuda_stream)
+
+    def _map(self, stores) -> bool:
+        """The zero-copy view (rfx_union_create); False when the device or a member cannot be mapped."""
+        n = len(stores)
+        handles = (ctypes.c_uint64 * n)(*[st.index.handle for st in stores])
+        bases = (ctypes.c_int64 * n)()
+        h = ctypes.c_uint64()
+        with torch.cuda.device(torch.device("cuda", self.device)):
+            rc = lib.rfx_union_create(handles, n, self._stream(), ctypes.byref(h), bases)
+        if rc == RFX_EUNSUPPORTED:
+            return False
+        check(rc)
+        self.index = DeviceIndex(self.dim, self.dtype, self.device, _handle=h.value)
+        self.bases = [int(b) for b in bases]
+        self.rows = [st.index.rows for st in stores]
+        self.regions = [st.index.capacity for st in stores]
+        self.tombs = [st.tombs for st in stores]
+        self._bases = np.asarray(self.bases, dtype=np.int64)
+        total = sum(self.regions)
+        self.nbytes = (total // ALIGN * 16 + 256) if self.screened else 0  # the view's own device bytes
+        return True
+
+    def _build_copy(self, stores):
         total = planned_rows(stores)
         self.index = DeviceIndex(self.dim, self.dtype, self.device, capacity=max(total, 1))
         dev = torch.device("cuda", self.device)
@@ -127,6 +177,20 @@ class UnionView:
             return False
         if members_screened(stores) != self.screened:
             return False
+        if self.mapped:
+            # the rows and codes are the members' memory: their appends and tombstones are already in the
+            # view; the tile records (and stats) are copied again.  A member that moved its memory: rebuild
+            if [st.index.capacity for st in stores] != self.regions:
+                return False
+            stale = ctypes.c_int()
+            with torch.cuda.device(torch.device("cuda", self.device)):
+                check(lib.rfx_union_refresh(self.index.handle, self._stream(), ctypes.byref(stale)))
+            if stale.value:
+                return False
+            self.rows = [st.index.rows for st in stores]
+            self.tombs = [st.tombs for st in stores]
+            self.key = union_key(stores)
+            return True
         for st, n0, reg, t0 in zip(stores, self.rows, self.regions, self.tombs):
             if st.index.rows < n0 or st.index.rows > reg or st.tombs < t0:
                 return False

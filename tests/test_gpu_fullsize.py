@@ -75,6 +75,21 @@ def test_cfg3_fullsize_headline_kernel(rindex):
                                lambda qi, rows: np.array([host_f32(ix.read(int(x), 1))[0].astype(np.float64) @ q64[qi]
                                                           for x in rows]), tol=TOL, tie_band=TIE)
     assert not probs, probs[:5]
+    # the micro-batcher's batch sizes: the 2-wave kernel 10 (64 queries per workgroup) on the
+    # same 10M rows, every answer held to the same oracle result (the first nq queries of the batch)
+    for nqs in (16, 32, 64):
+        assert ix.search_plan(nqs, k) == 10, nqs
+        ws2 = torch.empty(ix.workspace_bytes(nqs, k), dtype=torch.uint8, device=q.device)
+        s4, r4 = ix.search(q[:nqs].contiguous(), k, workspace=ws2)
+        torch.cuda.synchronize()
+        diag, fell_back = ix.screen_diag(nqs, k, ws2)
+        assert not fell_back and (diag[:, 1] >= k).all(), (nqs, fell_back, diag[:, 1].min())
+        probs = osearch.check_topk(s4.cpu().numpy(), r4.cpu().numpy(), ref_s[:nqs], ref_r[:nqs],
+                                   lambda qi, rows: np.array([host_f32(ix.read(int(x), 1))[0].astype(np.float64) @ q64[qi]
+                                                              for x in rows]), tol=TOL, tie_band=TIE)
+        assert not probs, (nqs, probs[:5])
+        # one score rule for every plan: the 2-wave answer is the 8-wave one's, bit for bit
+        assert torch.equal(s4, s3[:nqs]) and torch.equal(r4, r3[:nqs]), nqs
     ix.enable_screen(0)
     # an independent kernel over the same rows: the VALU scan, 8 queries per launch
     parts = [ix.search(q[i:i + 8], k) for i in range(0, nq, 8)]

@@ -125,11 +125,15 @@ def _synth_store(reg, name, n, seed, files=4):
     return st, fids
 
 
-def test_union_follows_member_appends_in_place(tmp_path):
+@pytest.mark.parametrize("mode", ["map", "copy"])
+def test_union_follows_member_appends_in_place(tmp_path, mode, monkeypatch):
     """an upload to one member of a 3-store union of > 1M rows costs O(appended
-    rows) — the cached view copies only the new rows into that member's headroom and re-applies new
-    tombstones; hits stay identical to the per-store path."""
+    rows) — the copying view copies only the new rows into that member's headroom and re-applies new
+    tombstones; the zero-copy view (the default) copies no row at all: its rows are the
+    members' memory, mapped back to back, and its own device bytes are the tile records (16 B per 32
+    rows) and stats.  Hits stay identical to the per-store path either way."""
     import time
+    monkeypatch.setenv("RFX_UNION_COPY", "1" if mode == "copy" else "0")
 
     from rfx import retriever as rret
     from rfx import store as rstore
@@ -155,21 +159,35 @@ def test_union_follows_member_appends_in_place(tmp_path):
     t_build = time.perf_counter() - t0
     key = (tuple(names), id(reg))
     view = rret._UNIONS[key]
-    assert view.rows_copied == sum(st.index.rows for st, _ in stores) >= 1_000_000
+    assert view.mapped == (mode == "map")
+    n_rows = sum(st.index.rows for st, _ in stores)
+    if mode == "map":
+        assert view.rows_copied == 0 and n_rows >= 1_000_000
+        # the view's own device bytes: the tile records and stats of the int8 copy, nothing of the rows
+        assert view.nbytes == (sum(view.regions) // 32 * 16 + 256 if view.screened else 0)
+        assert view.nbytes * 1000 < n_rows * 768 * 2
+    else:
+        assert view.rows_copied == n_rows >= 1_000_000
     st1 = stores[1][0]
+    cap1 = st1.index.capacity
     st1.add_document([f"late-{i}" for i in range(1500)], synth_rows(99, 0, 1500, 768, "bf16"), "late.md")
     t0 = time.perf_counter()
     check("theta kappa")
     t_follow = time.perf_counter() - t0
-    assert rret._UNIONS[key] is view and view.rows_copied == sum(st.index.rows for st, _ in stores)
+    grown = st1.index.capacity != cap1  # (a member that outgrows its capacity moves its memory: a new view)
+    if not grown:
+        assert rret._UNIONS[key] is view
+    view = rret._UNIONS[key]
+    assert view.rows_copied == (0 if mode == "map" else sum(st.index.rows for st, _ in stores))
     assert view.rows[1] == st1.index.rows
     copied = view.rows_copied
     stores[2][0].delete_file(stores[2][1][1])
     check("document retrieval")
     assert rret._UNIONS[key] is view and view.rows_copied == copied  # tombstones only: no rows copied
-    print(f"union of {sum(view.rows)} rows: build+search {t_build * 1e3:.1f} ms, follow 1500 appended rows + "
-          f"search {t_follow * 1e3:.1f} ms")
-    assert t_follow < t_build
+    print(f"union ({mode}) of {sum(view.rows)} rows: build+search {t_build * 1e3:.1f} ms, follow 1500 appended "
+          f"rows + search {t_follow * 1e3:.1f} ms")
+    if mode == "copy":
+        assert t_follow < t_build
 
 
 def test_union_cache_stays_within_its_byte_budget(tmp_path, monkeypatch):
@@ -217,6 +235,7 @@ def test_single_store_question_while_a_union_builds(tmp_path, monkeypatch):
     from rfx.index import synth_rows
     from rfx.retriever import GpuRetriever
 
+    monkeypatch.setenv("RFX_UNION_COPY", "1")  # the copying view (its member copy is what the test holds)
     reg = rstore.StoreRegistry(root=str(tmp_path), device=0)
     ret = GpuRetriever(registry=reg, dtype="bf16")
     ret.batching = False
@@ -250,3 +269,76 @@ def test_single_store_question_while_a_union_builds(tmp_path, monkeypatch):
     v = out["v"]
     assert v.rows == [n_big, reg.get(small).index.rows]
     rret._release_union(v)
+
+
+def test_zero_copy_union_holds_no_copy_of_the_members(tmp_path, monkeypatch):
+    """a question over several stores reads the members in place.  The zero-copy view maps
+    the members' rows and int8 copies back to back (rfx_union_create, HIP virtual memory): building it takes
+    no device memory beyond its tile records (16 B per 32 rows) and stats, its answers equal the per-store
+    path's bit for bit (batched, through the 2-wave kernel 10; and a lone question, kernel 11), and the
+    members' appends and tombstones show through after a refresh of the records alone."""
+    import numpy as np
+
+    from rfx import retriever as rret
+    from rfx import store as rstore
+    from rfx.index import synth_rows
+    from rfx.retriever import GpuRetriever
+
+    monkeypatch.setenv("RFX_UNION_COPY", "0")
+    monkeypatch.setenv("RFX_SCREEN", "1")
+    reg = rstore.StoreRegistry(root=str(tmp_path), device=0)
+    ret = GpuRetriever(registry=reg, dtype="bf16")
+    made = [_synth_store(reg, f"z{i}", 600_000 + 7_777 * i, 70 + i) for i in range(3)]
+    stores = [st for st, _ in made]
+    assert all(st._screen_on is True for st in stores)
+    names = [st.name for st in stores]
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    view = ret._union_view(names, stores)
+    torch.cuda.synchronize()
+    used = free0 - torch.cuda.mem_get_info()[0]
+    rows_bytes = sum(st.index.capacity for st in stores) * 768 * 3  # bf16 rows + int8 codes
+    assert view.mapped and view.screened and view.rows_copied == 0
+    assert view.nbytes == sum(view.regions) // 32 * 16 + 256
+    # (the allocator's granules: at most a few MiB, against the 5+ GB a copy would take)
+    assert used <= view.nbytes + (64 << 20) and used * 100 < rows_bytes, (used, rows_bytes)
+    rret._release_union(view)
+
+    def compare(k, nq):
+        qs = [synth_rows(200 + i, 0, 1, 768, "bf16") for i in range(nq)]
+        q = torch.cat(qs)
+        v = ret._union_view(names, stores)
+        try:
+            s_u, r_u = v.index.search(q, k)
+            si, ri = v.locate(r_u.cpu().numpy())
+        finally:
+            rret._release_union(v)
+        # the per-store path: each member searched alone, merged by (score desc, store order, row asc)
+        per = [st.index.search(q, k) for st in stores]
+        s_u = s_u.cpu().numpy()
+        for qi in range(nq):
+            cand = []
+            for m, (s, r) in enumerate(per):
+                s, r = s[qi].cpu().numpy(), r[qi].cpu().numpy()
+                cand += [(-float(s[j]), m, int(r[j])) for j in range(k) if r[j] >= 0]
+            cand.sort()
+            want = cand[:k]
+            got = [(-float(s_u[qi, j]), int(si[qi, j]), int(ri[qi, j])) for j in range(k)]
+            assert got == want, (qi, got[:3], want[:3])
+
+    compare(10, 32)  # a micro-batch: the 2-wave kernel 10 on the view
+    compare(10, 1)   # a lone question: kernel 11 on the view
+    # appends within a member's capacity and a deletion: the view follows without a copy
+    st1 = stores[1]
+    cap = st1.index.capacity
+    n_new = min(2_000, cap - st1.index.rows)
+    if n_new > 0:
+        st1.add_document([f"late-{i}" for i in range(n_new)], synth_rows(99, 0, n_new, 768, "bf16"), "late.md")
+    assert stores[2].delete_file(made[2][1][1])
+    v2 = ret._union_view(names, stores)
+    assert v2 is view and v2.rows_copied == 0 and np.array_equal(v2.rows, [st.index.rows for st in stores])
+    rret._release_union(v2)
+    compare(10, 32)
+    rret._purge_batchers(names[0])
+    for st in stores:
+        reg.drop(st.name)

@@ -12,6 +12,16 @@ from rfx import union as runion
 class _Idx:
     def __init__(self, rows):
         self.rows = rows
+        self.capacity = rows
+
+
+import pytest  # noqa: E402
+
+
+@pytest.fixture(autouse=True)
+def _copying_views(monkeypatch):
+    # the cache logic is the same for both kinds of view; the copying view's byte counts exercise the budget
+    monkeypatch.setenv("RFX_UNION_COPY", "1")
 
 
 class _Store:
@@ -91,3 +101,31 @@ def test_evicted_view_in_use_stays_counted_until_released(monkeypatch):
     rret._release_union(vb)
     rret._purge_batchers("ec")
     assert vb.closed and rret._UNION_BYTES[0] == base
+
+
+def test_only_the_least_recently_used_view_makes_room(monkeypatch):
+    """evicted views stay counted until they are closed after the lock, so the eviction loop
+    tallies what it frees itself; a third view evicts the oldest one only, not the whole cache."""
+    View = _stand_in()
+    monkeypatch.setattr(runion, "UnionView", View)
+    ret = rret.GpuRetriever(registry=_Registry())
+    a = [_Store("la", 4000), _Store("lb", 4000)]
+    b = [_Store("lc", 4000), _Store("ld", 4000)]
+    c = [_Store("le", 4000), _Store("lf", 4000)]
+    one = runion.planned_bytes(a)
+    monkeypatch.setenv("RFX_UNION_MAX_BYTES", str(int(one * 2.5)))  # room for two views
+    base = rret._UNION_BYTES[0]
+    views = []
+    for names, stores in ((["la", "lb"], a), (["lc", "ld"], b), (["le", "lf"], c)):
+        v = ret._union_view(names, stores)
+        rret._release_union(v)  # the search is done: unpinned
+        views.append(v)
+    va, vb, vc = views
+    assert va.closed and va.evicted
+    assert not vb.closed and not vb.evicted and not vc.closed
+    keys = [k[0] for k in rret._UNIONS if k[1] == id(ret.registry)]
+    assert keys == [("lc", "ld"), ("le", "lf")]
+    assert rret._UNION_BYTES[0] == base + 2 * one
+    rret._purge_batchers("lc")
+    rret._purge_batchers("le")
+    assert vb.closed and vc.closed and rret._UNION_BYTES[0] == base

@@ -63,9 +63,15 @@ for rnd in range(a.rounds):
 same = torch.equal(answers[True][0], answers[False][0]) and torch.equal(answers[True][1], answers[False][1])
 out = {"rows": a.rows, "devices": a.devices, "nq": a.nq, "k": a.k, "burst": a.burst,
        "plan": sidx.shards[0].search_plan(a.nq, a.k), "c_equals_python": bool(same)}
+# On a real node the shards run side by side, one per GPU: a step's GPU time is ONE shard's, which this box
+# (all shards on one GPU, run one after another) approximates by the serial time / the shard count (VERDICT r5
+# weak #6: the host issue is judged against that).
+nsh = len(sidx.shards)
 for key, v in res.items():
-    out[key] = {"host_issue_ms": round(min(x[0] for x in v), 4), "gpu_ms_per_search": round(min(x[1] for x in v), 4),
-                "issue_over_gpu": round(min(x[0] for x in v) / min(x[1] for x in v), 3)}
+    issue, gpu = min(x[0] for x in v), min(x[1] for x in v)
+    out[key] = {"host_issue_ms": round(issue, 4), "gpu_ms_per_search": round(gpu, 4),
+                "per_shard_gpu_ms": round(gpu / nsh, 4), "issue_over_shard_gpu": round(issue / (gpu / nsh), 3)}
+out["issue_threads"] = os.environ.get("RFX_ISSUE_THREADS", "default (pool)")
 print(json.dumps(out, indent=1))
 if not same:
     sys.exit("the C path's answer differs from the Python path's")
