@@ -18,8 +18,11 @@ RFX_K10_DECL(launch_768)
 RFX_K10_DECL(launch_1024)
 RFX_K10_DECL(launch_768_w2)
 RFX_K10_DECL(launch_1024_w2)
-#undef RFX_K10_DECL
 }  // namespace k10
+namespace k10q {
+RFX_K10_DECL(launch_768)
+}  // namespace k10q
+#undef RFX_K10_DECL
 
 namespace {
 
@@ -507,6 +510,16 @@ void launch_screen_quantize(const void* X, int D, int dtype, int64_t tile0, int6
 // config.py:137, chat.py:496-521) run the 2-wave kernel: 64 queries per workgroup, two workgroups per CU,
 // 512 workgroups over the corpus (fewer on a small store: >= 8 tiles each).  Larger batches the 8-wave
 // kernel (256 queries per workgroup, one per CU).  RFX_SCREEN_W2_BLOCKS (tuning) overrides the former's count.
+// RFX_K10_Q64=1: batches of more than 64 questions at d 768 run the 64-queries-per-wave kernel
+// (k_scan_screen64.h: 4 waves x 64 queries, one list per query per workgroup) instead of the 8-wave one
+bool screen_q64() {
+  static const bool v = [] {
+    const char* e = getenv("RFX_K10_Q64");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 int screen_w2_blocks() {
   static const int v = [] {
     const char* e = getenv("RFX_SCREEN_W2_BLOCKS");
@@ -537,8 +550,8 @@ MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k, in
   ranges = std::max<int64_t>(std::min<int64_t>(ranges, ntiles), 1);
   p.blocks = (int)ranges;
   p.tiles_per_block = (int)((ntiles + ranges - 1) / ranges);
-  p.lists_per_block = 2;
-  p.n_lists = (int64_t)p.blocks * 2;
+  p.lists_per_block = (!w2 && D == 768 && screen_q64()) ? 1 : 2;  // (the 64-queries-per-wave kernel: one list)
+  p.n_lists = (int64_t)p.blocks * p.lists_per_block;
   return p;
 }
 
@@ -585,7 +598,8 @@ int launch_scan_screen(const MfmaPlan& p, const int8_t* codes, const void* tmeta
   const int ntiles = (nrows + k10::kTM - 1) / k10::kTM;
   dim3 grid(p.blocks, p.q_blocks);
   auto f = p.bn == k10::kQGSmall ? (D == 768 ? k10::launch_768_w2 : k10::launch_1024_w2)
-                                 : (D == 768 ? k10::launch_768 : k10::launch_1024);
+           : p.lists_per_block == 1 ? k10q::launch_768
+                                    : (D == 768 ? k10::launch_768 : k10::launch_1024);
   return f(p.k_lane, grid, st, codes, (const uint4*)tmeta, stats, Qc, qe2, nq, ntiles, tau, cs, cr, drops, p.n_lists,
            mask, tau + p.nq_pad * k10::kTauW, xcd_weights_device_ptr());
 }

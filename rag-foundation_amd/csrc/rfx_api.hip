@@ -72,6 +72,10 @@ struct Phys {
     if (bytes) (void)hipMemRelease(h);
   }
 };
+// An address range is never freed, only unmapped: measured on the box (tools/r06/vmm_probe3.hip), a range that
+// is freed and reserved again (the runtime hands back the same address) and mapped to NEW physical memory is
+// written wrongly by hipMemcpy host-to-device copies — 19 of 40 rounds had 1.5M of 4M words stale — while fresh
+// addresses were right in 40 of 40.  Unmapped ranges cost address space only (a store's growth is geometric).
 struct Mapping {
   void* va = nullptr;
   size_t bytes = 0;
@@ -82,7 +86,6 @@ struct Mapping {
       (void)hipMemUnmap((uint8_t*)va + off, p->bytes);
       off += p->bytes;
     }
-    if (va) (void)hipMemAddressFree(va, bytes);
   }
 };
 
@@ -124,6 +127,7 @@ int vmm_map(int device, const std::vector<std::shared_ptr<Phys>>& parts, std::sh
     m->va = nullptr;
     return fail(RFX_ENOMEM, "hipMemAddressReserve(%zu) failed", m->bytes);
   }
+  // (never freed: see Mapping)
   size_t off = 0;
   for (auto& p : parts) {
     if (hipMemMap((uint8_t*)m->va + off, p->bytes, 0, p->h, 0) != hipSuccess)

@@ -192,7 +192,9 @@ def test_union_follows_member_appends_in_place(tmp_path, mode, monkeypatch):
 
 def test_union_cache_stays_within_its_byte_budget(tmp_path, monkeypatch):
     """The view cache is bounded in bytes (RFX_UNION_MAX_BYTES, LRU), not by a count; a list whose view
-    alone exceeds the budget takes the per-store path."""
+    alone exceeds the budget takes the per-store path.  (Copying views: a zero-copy view holds only its tile
+    records, which no realistic budget excludes.)"""
+    monkeypatch.setenv("RFX_UNION_COPY", "1")
     from rfx import retriever as rret
     from rfx import store as rstore
     from rfx import union as runion
