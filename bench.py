@@ -410,7 +410,8 @@ def main():
             blocks = max(min(blocks // 8 * 8 if blocks > 8 else blocks, ntiles), 1)
         else:
             blocks = min(256 // max(1, nq_pad // 256), ntiles)
-        n_lists = 2 * blocks
+        # lists per (query, workgroup): 2 (32 queries per wave), 1 with the 64-queries-per-wave kernel (RFX_K10_Q64)
+        n_lists = (1 if (a.nq > 64 and a.dim == 768 and os.environ.get("RFX_K10_Q64") == "1") else 2) * blocks
         kl = 4 if a.k <= 4 else 10
         alg_bytes = (n_max * a.dim + (-(-n_max // 32)) * 16 + nq_pad * a.dim + nq_pad * 4
                      + a.nq * n_lists * (kl * 8 + 4))
