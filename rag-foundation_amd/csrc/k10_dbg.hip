@@ -17,6 +17,11 @@
 #include "k_scan_screen.h"
 
 namespace rfx {
+namespace k10q {
+int launch_768(int kl, dim3 grid, hipStream_t st, const int8_t* X, const uint4* tm, const uint32_t* sts, const int8_t* Qc,
+               const float* qe2, int nq, int ntiles, uint32_t* tau, float* cs, int* cr, uint32_t* dr, int64_t n_lists,
+               const uint32_t* mask, uint32_t* xb, uint32_t* xw);
+}  // namespace k10q
 
 int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, const void* tmv, const uint32_t* sts,
                            int nrows, const int8_t* Qc, const float* qe2, int nq, uint32_t* tau, float* cs, int* cr,
@@ -32,41 +37,19 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
                        xcd_weights_device_ptr());                                                             \
     break;
   switch (variant) {
-    // (round 5 trimmed the list to the variants its tools run; earlier rounds' ring and MODE sweeps are in
-    // the profiles they wrote)
-    RFX_K10V(8, 0)
-    RFX_K10V(8, 1)
-    RFX_K10V(8, 8)
-    RFX_K10V(8, 9)
-    RFX_K10V(8, 32)
-    RFX_K10V(8, 512)
-    RFX_K10V(8, 4096)
-    RFX_K10V(8, 8192)
-    RFX_K10V(8, 65536)
-    RFX_K10V(8, 4096 + 65536)
-    RFX_K10V(8, 524288)
-    RFX_K10V(8, 1048576)
-    RFX_K10V(8, 1048576 + 8192)
-    RFX_K10V(12, 0)
-    RFX_K10V(12, 2097152)
-    RFX_K10V(12, 2097152 + 8192)
-    RFX_K10V(12, 2097152 + 65536)
-    RFX_K10V(12, 2097152 + 524288)
-    RFX_K10V(12, 2097152 + 1048576)
-    RFX_K10V(10, 2097152)
-    RFX_K10V(10, 2097152 + 8192)
-    RFX_K10V(10, 2097152 + 512)
-    RFX_K10V(10, 2097152 + 1)
-    RFX_K10V(10, 2097152 + 4194304)
-    RFX_K10V(10, 2097152 + 4194304 + 8192)
-    RFX_K10V(10, 2097152 + 16384)
-    RFX_K10V(10, 2097152 + 16384 + 8192)
+    // (round 6 trimmed the list to the variants its tools run: production, no fold (1), no fold and no stream
+    // (9), slow path never taken (512), the trips counter (8192) and the block clocks (65536); earlier rounds'
+    // sweeps are in the profiles they wrote)
     RFX_K10V(10, 2097152 + 8388608)
-    RFX_K10V(10, 2097152 + 8388608 + 8192)
-    RFX_K10V(10, 2097152 + 8388608 + 512)
     RFX_K10V(10, 2097152 + 8388608 + 1)
-    RFX_K10V(12, 2097152 + 1)
-    RFX_K10V(12, 2097152 + 512)
+    RFX_K10V(10, 2097152 + 8388608 + 9)
+    RFX_K10V(10, 2097152 + 8388608 + 512)
+    RFX_K10V(10, 2097152 + 8388608 + 8192)
+    RFX_K10V(10, 2097152 + 8388608 + 65536)
+    case 64:  // the 64-queries-per-wave kernel (k_scan_screen64.h; its plan: RFX_K10_Q64=1, one list per workgroup)
+      if (p.lists_per_block != 1) return -1;
+      return k10q::launch_768(10, grid, st, X, tm, sts, Qc, qe2, nq, ntiles, tau, cs, cr, dr, p.n_lists, nullptr,
+                              tau + p.nq_pad * k10::kTauW, xcd_weights_device_ptr());
     default:
       return -1;
   }

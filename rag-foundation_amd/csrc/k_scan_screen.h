@@ -61,8 +61,9 @@ constexpr int kMR = 8;  // tile-metadata slots (1 KB each: 64 lane copies of the
 constexpr int kXbWords = 8;  // after the slot table: the XCD split's weight snapshot for this launch
 #ifdef RFX_K10_BLOCK_TIMES
 // debug build only (k10_dbg.hip): MODE 65536 records each block's 100-MHz wall clock when it starts
-// and when all its waves are done (tools/k10_variants.py --block-times)
-__device__ unsigned long long g_k10_bt[1024][2];
+// and when all its waves are done ([0], [1]), and its shader clock (s_memtime) at the same points ([2], [3]):
+// the in-kernel clock = d(memtime) / d(realtime) x 100 MHz (tools/k10_block_times.py)
+__device__ unsigned long long g_k10_bt[1024][4];
 // MODE 8192: per tile index (capped at 63) the wave-tiles that enter the slow path and the pop-loop
 // trips they make (max over the wave's lanes of the passing values), summed over all waves
 __device__ unsigned int g_k10_trips[2][64];
@@ -540,7 +541,10 @@ __global__ __launch_bounds__(64 * NW, 1) void scan_screen_kernel(const int8_t* _
   if (S == 0) return;
 #ifdef RFX_K10_BLOCK_TIMES
   if constexpr ((MODE & 65536) != 0)
-    if (tid == 0 && range < 1024 && blockIdx.y == 0) g_k10_bt[range][0] = wall_clock64();
+    if (tid == 0 && range < 1024 && blockIdx.y == 0) {
+      g_k10_bt[range][0] = wall_clock64();
+      g_k10_bt[range][2] = __builtin_amdgcn_s_memtime();
+    }
 #endif
   const int lst = range * 2 + half;
   const float e2 = qe2[q];
@@ -1032,7 +1036,10 @@ __global__ __launch_bounds__(64 * NW, 1) void scan_screen_kernel(const int8_t* _
   if constexpr ((MODE & 65536) != 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0 && range < 1024 && blockIdx.y == 0) g_k10_bt[range][1] = wall_clock64();
+    if (tid == 0 && range < 1024 && blockIdx.y == 0) {
+      g_k10_bt[range][1] = wall_clock64();
+      g_k10_bt[range][3] = __builtin_amdgcn_s_memtime();
+    }
   }
 #endif
 }

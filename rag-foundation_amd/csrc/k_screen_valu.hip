@@ -462,15 +462,33 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   if (!INL && !lastu) return;
   if (!lastu) {
     // wait for the last block's verdict on this launch, at most kVerdictWait of wall clock (100 MHz):
-    // a block that stops waiting exits, and the fallback completes without it
+    // a block that stops waiting exits, and the fallback completes without it.  Round 6: every
+    // 8th poll also reads the arrival counter; while blocks are still to arrive and none has for kStallWait,
+    // the grid is not all running (another launch holds CUs: a kernel-10 batch, a second kernel-11 launch) and
+    // this block leaves at once, so the late blocks find a CU.  The counter reads 0 only once the last block
+    // has reset it, right before its verdict.  Worst case a waiting block holds its CU for kVerdictWait when
+    // every block has arrived and the last block's check runs long; for kStallWait + one poll (~6 us) when
+    // arrivals stall.
     constexpr uint64_t kVerdictWait = 5000;  // 50 us
+    constexpr uint64_t kStallWait = 500;     // 5 us
     __shared__ uint32_t verdict;
     if (tid == 0) {
       const uint64_t t0 = wall_clock64();
-      uint32_t d = 0u;
-      for (;;) {
+      uint64_t t_seen = t0;
+      uint32_t d = 0u, seen = 0xffffffffu;
+      for (int i = 1;; ++i) {
         d = __hip_atomic_load(dec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (((d >> 2) == (gen0 & 0x3fffffffu) && (d & 3u)) || wall_clock64() - t0 > kVerdictWait) break;
+        const uint64_t now = wall_clock64();
+        if (((d >> 2) == (gen0 & 0x3fffffffu) && (d & 3u)) || now - t0 > kVerdictWait) break;
+        if ((i & 7) == 0) {
+          const uint32_t c = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (c != seen) {
+            seen = c;
+            t_seen = now;
+          } else if (c != 0u && c < gridDim.x && now - t_seen > kStallWait) {
+            break;
+          }
+        }
         __builtin_amdgcn_s_sleep(8);
       }
       verdict = (d >> 2) == (gen0 & 0x3fffffffu) ? (d & 3u) : 0u;

@@ -1590,7 +1590,7 @@ int rfx_dbg_select_times(unsigned long long* out_h) {
 }
 
 // Diagnostic: kernel 10's per-block wall clocks of the last MODE-65536 variant launch (k10_dbg.hip
-// g_k10_bt: [1024][2] u64 start / end, 100 MHz).
+// g_k10_bt: [1024][4] u64: wall clock start / end (100 MHz), shader clock start / end).
 int rfx_dbg_k10_block_times(unsigned long long* out_h) {
   if (!out_h) return fail(RFX_EINVAL, "null out");
   if (rfx::dbg_k10_block_times(out_h) != 0) return fail(RFX_EDEVICE, "hipMemcpyFromSymbol failed");

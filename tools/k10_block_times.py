@@ -6,6 +6,7 @@ median block and of the last block relative to the first start."""
 import argparse
 import ctypes
 import json
+import time
 import os
 import sys
 
@@ -24,7 +25,9 @@ ap.add_argument("--rows", type=int, default=1_250_000)
 ap.add_argument("--nq", type=int, default=256)
 ap.add_argument("--k", type=int, default=10)
 ap.add_argument("--reps", type=int, default=20)
-ap.add_argument("--variant", type=int, default=800065536, help="800065536 = round 4 schedule + clocks; 800069632 = static split (10**8 * RING + MODE)")
+ap.add_argument("--variant", type=int, default=1010551296,
+                help="1010551296 = production (RING 10, per-tile barrier, publish on change) + clocks (10**8 * RING + MODE)")
+ap.add_argument("--warm-seconds", type=float, default=3.0, help="back-to-back launches first (the clock under load)")
 a = ap.parse_args()
 f = _lib.lib.rfx_dbg_screen_variant
 f.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
@@ -41,13 +44,20 @@ ws = torch.empty(ix.workspace_bytes(a.nq, a.k), dtype=torch.uint8, device="cuda"
 st = _lib.stream_ptr()
 ntiles = -(-a.rows // 32)
 recs = []
+t_end = time.time() + a.warm_seconds
+while time.time() < t_end:
+    for _ in range(20):
+        _lib.check(f(ix.handle, _lib.ptr(q), a.nq, a.k, a.variant, _lib.ptr(ws), ws.numel(), st))
+    torch.cuda.synchronize()
 for rep in range(a.reps):
     _lib.check(f(ix.handle, _lib.ptr(q), a.nq, a.k, a.variant, _lib.ptr(ws), ws.numel(), st))
     torch.cuda.synchronize()
-    bt = np.zeros((1024, 2), dtype=np.uint64)
+    bt = np.zeros((1024, 4), dtype=np.uint64)
     _lib.check(g(bt.ctypes.data))
     nb = min(256, ntiles)
-    t = bt[:nb].astype(np.int64) * 10  # ns
+    t = bt[:nb, :2].astype(np.int64) * 10  # ns
+    ck = bt[:nb, 2:].astype(np.int64)  # shader clock ticks
+    clk_mhz = (ck[:, 1] - ck[:, 0]) / np.maximum(t[:, 1] - t[:, 0], 1) * 1e3
     t0 = t[:, 0].min()
     dur = t[:, 1] - t[:, 0]
     ends = t[:, 1] - t0
@@ -56,7 +66,7 @@ for rep in range(a.reps):
                  "start_skew_ns": int(t[:, 0].max() - t0), "dur_med_ns": int(np.median(dur)),
                  "dur_p90_ns": int(np.percentile(dur, 90)), "dur_max_ns": int(dur.max()),
                  "end_med_ns": int(np.median(ends)), "end_max_ns": int(ends.max()),
-                 "tail_ns": int(ends.max() - np.median(ends))})
+                 "tail_ns": int(ends.max() - np.median(ends)), "clock_mhz_med": int(np.median(clk_mhz))})
 keys = [k for k in recs[0] if k not in ("xcd_dur_med_ns", "slowest_blocks")]
 med = {k: int(np.median([r[k] for r in recs[a.reps // 4:]])) for k in keys}
 med["xcd_dur_med_ns"] = [int(x) for x in np.median([r["xcd_dur_med_ns"] for r in recs[a.reps // 4:]], axis=0)]

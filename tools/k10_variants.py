@@ -77,6 +77,7 @@ if a.rounds == 0:
     sys.exit(0)
 if a.seconds > 0:  # steady state of ONE variant (rocm-smi samples power / sclk meanwhile)
     v = variants[0]
+    print(f"burst start {v}", file=sys.stderr, flush=True)  # (tools/r06/gpu_power.sh samples rocm-smi from here)
     n, t0 = 0, time.time()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
