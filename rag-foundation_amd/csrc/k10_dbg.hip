@@ -14,7 +14,7 @@
 // via rfx_dbg_screen_variant; variant = 10^8 * RING + MODE (RING in {4, 6, 8, 10, 12}; round 5's first
 // sessions used 10^7 * RING + MODE, rounds 3-4 100000 * RING + MODE).
 #define RFX_K10_BLOCK_TIMES
-#include "k_scan_screen.h"
+#include "k_scan_screen64.h"
 
 namespace rfx {
 namespace k10q {
@@ -50,6 +50,18 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
       if (p.lists_per_block != 1) return -1;
       return k10q::launch_768(10, grid, st, X, tm, sts, Qc, qe2, nq, ntiles, tau, cs, cr, dr, p.n_lists, nullptr,
                               tau + p.nq_pad * k10::kTauW, xcd_weights_device_ptr());
+    case 65:  // the same, slow path never taken (timing)
+    case 73:  // the same, no fold and no corpus stream (timing)
+      if (p.lists_per_block != 1) return -1;
+      if (variant == 65)
+        hipLaunchKernelGGL((k10q::scan_screen_q64_kernel<10, 768, false, k10q::kRing768, 1>), grid, dim3(256), 0, st, X,
+                           tm, sts, Qc, qe2, nq, ntiles, tau, cs, cr, dr, p.n_lists, nullptr, tau + p.nq_pad * k10::kTauW,
+                           xcd_weights_device_ptr());
+      else
+        hipLaunchKernelGGL((k10q::scan_screen_q64_kernel<10, 768, false, k10q::kRing768, 9>), grid, dim3(256), 0, st, X,
+                           tm, sts, Qc, qe2, nq, ntiles, tau, cs, cr, dr, p.n_lists, nullptr, tau + p.nq_pad * k10::kTauW,
+                           xcd_weights_device_ptr());
+      break;
     default:
       return -1;
   }

@@ -114,8 +114,9 @@ __device__ __forceinline__ void fold_trip32(const v4i32 (&a)[8], float st, int r
 }
 
 // X, tmeta, stats, Qc, qe2, tau, xb, xw: as kernel 10.  Outputs per (query, list = workgroup): KL candidates
-// (A, row) best first (empty tail -inf / kEmptyRow) and the list's drop.
-template <int KL, int D, bool MASK, int RING>
+// (A, row) best first (empty tail -inf / kEmptyRow) and the list's drop.  MODE (debug library only, timing;
+// wrong results): 1 = the slow path compiled in, never taken; 8 = no corpus stream after the prologue.
+template <int KL, int D, bool MASK, int RING, int MODE = 0>
 __global__ __launch_bounds__(256, 1) void scan_screen_q64_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                                  const uint32_t* __restrict__ stats,
                                                                  const int8_t* __restrict__ Qc, const float* __restrict__ qe2,
@@ -291,6 +292,7 @@ __global__ __launch_bounds__(256, 1) void scan_screen_q64_kernel(const int8_t* _
     bool hit = false;
 #pragma unroll
     for (int qb = 0; qb < 4; ++qb) hit = hit || (float)m[qb] * st_t >= tfq[qb];
+    if constexpr ((MODE & 1) != 0) hit = hit && nq < 0;
     if (__builtin_amdgcn_ballot_w64(hit)) {
       const uint2 md = *(const uint2*)(lds + kMetaOff + (it % kMR) * 1024 + lane * 16);
       const float st = __uint_as_float(md.x);
@@ -336,11 +338,15 @@ __global__ __launch_bounds__(256, 1) void scan_screen_q64_kernel(const int8_t* _
       const int slot = g % RING;
 #pragma unroll
       for (int kk = 0; kk < KPS; ++kk) {
-        if (kk == 0) {
-          const int h = g + AHEAD;
-          issue_piece(h, h % RING);
-        }
-        if (kk == KB && s == NST - 1) {
+        if constexpr ((MODE & 8) == 0)
+          if (kk == 0) {
+            const int h = g + AHEAD;
+            issue_piece(h, h % RING);
+          }
+        if (kk == KB && s == NST - 1 && (MODE & 8) != 0) {
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          asm volatile("s_barrier" ::: "memory");
+        } else if (kk == KB && s == NST - 1) {
           // tile it + 1 landed: younger are the pieces of stages NST (it + 2) .. NST it + RING - 1, their records,
           // and the refreshes issued after the last needed piece (tiles it + 2 - TBD .. it - 1)
           constexpr int NMY = (RING - NST - 1) / NST;

@@ -2,7 +2,8 @@
 # Round 6 (first step): package power and sclk (rocm-smi) during 16-s bursts of kernel 10
 # variants on config 3 (10M x 768, nq 256), and the in-kernel clock of production from per-block
 # s_memtime / s_memrealtime stamps (debug MODE 65536).  Variants (10^8 RING + MODE): production 1010485760,
-# no fold 1010485761, no fold + no corpus stream 1010485769, and 64 = the 64-queries-per-wave kernel.
+# no fold 1010485761, no fold + no corpus stream 1010485769; the 64-queries-per-wave kernel: 64, its
+# no-fold 65 and no-fold-no-stream 73.
 set -o pipefail
 O=${1:-gpurun_out/r06p}
 mkdir -p "$O"
@@ -17,8 +18,8 @@ sample() {  # $1 = output file: rocm-smi every ~0.5 s while the burst runs
     sleep 0.5
   done
 }
-for v in 1010485760 1010485761 1010485769 64; do
-  [ "$v" = "64" ] && export RFX_K10_Q64=1 || unset RFX_K10_Q64
+for v in 1010485760 1010485761 1010485769 64 65 73; do
+  [ "$v" -lt 100 ] && export RFX_K10_Q64=1 || unset RFX_K10_Q64
   timeout -k 10 200 python -u tools/k10_variants.py --variants $v --seconds 16 --rounds 1 --burst 5 > "$O/run_$v.json" 2> "$O/run_$v.err" &
   pid=$!
   for i in $(seq 1 240); do grep -q "burst start" "$O/run_$v.err" 2>/dev/null && break; sleep 0.5; done
