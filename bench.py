@@ -406,7 +406,7 @@ def main():
         ntiles = -(-n_max // 32)
         if a.nq <= 64:  # the 2-wave kernel (k_screen.hip plan_scan_screen): 64 queries, up to 512 workgroups
             nq_pad = 64
-            blocks = min(int(os.environ.get("RFX_SCREEN_W2_BLOCKS", "0")) or 512, max(ntiles // 8, 8))
+            blocks = min(int(os.environ.get("RFX_SCREEN_W2_BLOCKS", "0")) or 512, max(ntiles // 12, 8))
             blocks = max(min(blocks // 8 * 8 if blocks > 8 else blocks, ntiles), 1)
         else:
             blocks = min(256 // max(1, nq_pad // 256), ntiles)

@@ -542,7 +542,10 @@ MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k, in
   int64_t ranges;
   if (w2) {
     ranges = max_blocks > 0 ? max_blocks : screen_w2_blocks() > 0 ? screen_w2_blocks() : 512;
-    ranges = std::min<int64_t>(ranges, std::max<int64_t>(ntiles / 8, 8));
+    // >= ~12 tiles per workgroup: each block's first tiles pass nearly every value (its bound is not there
+    // yet), so a small store wants fewer, longer blocks (100k x 768 f32, nq 32: 256 blocks 0.079 ms, 384
+    // blocks 0.104 ms, 128 blocks 0.082 ms; profiles/r06/tune/)
+    ranges = std::min<int64_t>(ranges, std::max<int64_t>(ntiles / 12, 8));
     if (ranges > 8) ranges = ranges / 8 * 8;  // (a multiple of 8: the XCD-balanced split)
   } else {
     ranges = std::max<int64_t>((max_blocks > 0 ? max_blocks : 256) / std::max(p.q_blocks, 1), 1);
