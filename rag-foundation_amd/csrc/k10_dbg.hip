@@ -46,6 +46,7 @@ int launch_scan_screen_dbg(const MfmaPlan& p, int variant, const int8_t* X, cons
     RFX_K10V(10, 2097152 + 8388608 + 512)
     RFX_K10V(10, 2097152 + 8388608 + 8192)
     RFX_K10V(10, 2097152 + 8388608 + 65536)
+    RFX_K10V(10, 2097152 + 8388608 + 33554432)  // one wave DMAs the tile records (round 6 A/B)
     case 64:  // the 64-queries-per-wave kernel (k_scan_screen64.h; its plan: RFX_K10_Q64=1, one list per workgroup)
       if (p.lists_per_block != 1) return -1;
       return k10q::launch_768(10, grid, st, X, tm, sts, Qc, qe2, nq, ntiles, tau, cs, cr, dr, p.n_lists, nullptr,

@@ -476,6 +476,9 @@ constexpr int kModeTileBarrier = 2097152;  // one wait + barrier per tile (TB be
 constexpr int kModeFloatMask = 4194304;  // the slow path's float pass mask (fold_mask) instead of fold_mask_int
 constexpr int kModePubOnChange = 8388608;  // publish a list's best only when it rose (production; variant encoding 10^8 RING + MODE)
 constexpr int kModeSortMerge = 16384;  // a wave with >= 8 passes in some lane folds by one sorted merge (debug)
+// round 6 (debug A/B): only wave 0 DMAs each tile's 16-B record (1 KB: 64 lane copies) instead of all 8 waves
+// (the per-tile barrier makes it visible to every wave); the other waves' counted waits drop the records
+constexpr int kModeMetaOne = 33554432;
 template <int KL, int D, bool MASK, int RING = kRing, int MODE = 0, int NW = kWaves>
 __global__ __launch_bounds__(64 * NW, 1) void scan_screen_kernel(const int8_t* __restrict__ X, const uint4* __restrict__ tmeta,
                                                              const uint32_t* __restrict__ stats,
@@ -600,6 +603,9 @@ __global__ __launch_bounds__(64 * NW, 1) void scan_screen_kernel(const int8_t* _
   // first stage, every wave also DMAs the tile's 16-B record (64 lane copies, identical bytes from
   // every wave) into meta slot (tile % kMR), read by the epilogue's slow path from LDS.
   const v4i32 meta_rsrc = make_rsrc(tmeta);
+  // (per-tile barrier schedule only: see kModeMetaOne)
+  constexpr bool META1 = (MODE & kModeMetaOne) != 0 && (MODE & kModeTileBarrier) != 0 && (MODE & 32768) == 0 &&
+                         (MODE & 8) == 0;
   auto issue_piece = [&](int gi, int slot) {
     const bool first = gi % NST == 0;  // (counted on the unclamped index: the waits stay exact)
     gi = gi < S ? gi : S - 1;  // tail: harmless duplicate loads keep the counted waits exact
@@ -613,7 +619,7 @@ __global__ __launch_bounds__(64 * NW, 1) void scan_screen_kernel(const int8_t* _
           __builtin_amdgcn_readfirstlane(lds_base + (uint32_t)(slot * kSlot) + (uint32_t)((w + NW * u) * 1024));
       bdma_nt(rs, laneoff[u], dst);  // codes are read once per batch
     }
-    if (first) {
+    if (first && (!META1 || w == 0)) {
       const uint32_t mdst = __builtin_amdgcn_readfirstlane(lds_base + kMetaOff + (uint32_t)((ti % kMR) * 1024));
       bdma(meta_rsrc, (uint32_t)tile_of(ti) * 16u, mdst);
     }
@@ -724,7 +730,10 @@ __global__ __launch_bounds__(64 * NW, 1) void scan_screen_kernel(const int8_t* _
   if constexpr (TB) {
     // tile 0 landed: younger are the pieces of stages NST .. AHEAD - 1 and their tile records
     constexpr int NMT = (AHEAD - 1) / NST;  // records of stages NST, 2 NST, ... <= AHEAD - 1
-    asm volatile("s_waitcnt vmcnt(%0)" ::"i"((AHEAD - NST) * GPW + NMT) : "memory");
+    if (META1 && w != 0)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"((AHEAD - NST) * GPW) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"((AHEAD - NST) * GPW + NMT) : "memory");
   } else {
     // stage 0 landed: younger are stages 1 .. AHEAD - 1 and the metadata records issued with stages
     // 0 .. AHEAD - 1 (with piece 0's own record after it)
@@ -901,15 +910,28 @@ __global__ __launch_bounds__(64 * NW, 1) void scan_screen_kernel(const int8_t* _
 #pragma unroll
             for (int d = 1; d <= TBD - 2; ++d) nt_ += (it >= d && tau_refresh_tile<MODE>(it - d)) ? kTauGPW : 0;
             static_assert(kTauGPW == 2, "wait table below");
-            switch (nt_) {
+            if (META1 && w != 0) {  // (this wave issued no tile records)
+              switch (nt_) {
+#define RFX_K10_TWAIT(N)                                                                                      \
+  case N:                                                                                                     \
+    asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"((RING - 2 * NST) * GPW + N) : "memory");               \
+    break;
+                RFX_K10_TWAIT(0) RFX_K10_TWAIT(2)
+                default:  // stricter, never looser
+                  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"((RING - 2 * NST) * GPW) : "memory");
+#undef RFX_K10_TWAIT
+              }
+            } else {
+              switch (nt_) {
 #define RFX_K10_TWAIT(N)                                                                                      \
   case N:                                                                                                     \
     asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"((RING - 2 * NST) * GPW + NMY + N) : "memory");         \
     break;
-              RFX_K10_TWAIT(0) RFX_K10_TWAIT(2)
-              default:  // stricter, never looser
-                asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"((RING - 2 * NST) * GPW + NMY) : "memory");
+                RFX_K10_TWAIT(0) RFX_K10_TWAIT(2)
+                default:  // stricter, never looser
+                  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"i"((RING - 2 * NST) * GPW + NMY) : "memory");
 #undef RFX_K10_TWAIT
+              }
             }
             asm volatile("s_barrier" ::: "memory");
             if (tau_refresh_tile<MODE>(it)) issue_tau();
