@@ -498,35 +498,6 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     return;
   }
   RFX_K11_L(0);
-  // The last block's own record entries (round 6): it never ran the early re-score, so a
-  // survivor of its own record cost a round of cold row loads on the critical path (49 % of searches,
-  // round 5).  Their rows are loaded here, the records' loads queue behind them, and they are re-scored as
-  // soon as the first query's records have landed.  One pass of 16 rows (a lone question's record has at
-  // most 15); any others take the re-score below as before.
-  constexpr int ESZL = DT == RFX_F32 ? 4 : 2;
-  constexpr int VPLL = D * ESZL / 256;
-  uint4 oxv[VPLL], oyv[VPLL];
-  int o_qi = 0, o_e = 0, o_tot = 0;
-  const bool own = !(force & 16) && !(force & 8);
-  if (own) {
-    for (int qi = 0; qi < nq; ++qi) o_tot += nxl[qi];
-    o_tot = __builtin_amdgcn_readfirstlane(o_tot);
-    if (o_tot > 0) {
-      const int grp = tid >> 4, gl = tid & 15;
-      int e = grp < o_tot ? grp : 0;  // (clamped: whole 16-lane rows take part in the sum)
-      while (o_qi < nq - 1 && e >= nxl[o_qi]) {
-        e -= nxl[o_qi];
-        ++o_qi;
-      }
-      o_e = e;
-      const int r = xrow[o_qi][o_e];
-#pragma unroll
-      for (int u = 0; u < VPLL; ++u) {
-        oyv[u] = *(const uint4*)((const uint8_t*)Q + (int64_t)o_qi * D * ESZL + (int64_t)(gl + 16 * u) * 16);
-        oxv[u] = *(const uint4*)((const uint8_t*)X + (int64_t)r * D * ESZL + (int64_t)(gl + 16 * u) * 16);
-      }
-    }
-  }
   if (force & 8) {
     if (tid == 0) {
       *gate = 0u;
@@ -581,13 +552,6 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       n_mv = 0;
     }
     __syncthreads();
-    if (qi == 0 && o_tot > 0) {  // the own entries' exact keys (their rows were loaded before the records)
-      const double acc = exact_dot16<DT, VPLL>(oxv, oyv);
-      if ((tid & 15) == 0 && (tid >> 4) < o_tot)
-        __hip_atomic_store(cand_x + ((int64_t)o_qi * n_lists + blockIdx.x) * kK + o_e, ord_f32((float)acc),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (read back by this block's survivor step)
-    }
     if (qi == 0) RFX_K11_L(1);
     // The largest drop bound (entry 15 of each record), and LB, a lower bound of a_k: the k-th largest
     // key (with multiplicity; 0 = fewer than k) of the records' best entries (every entry when the
