@@ -676,6 +676,12 @@ __global__ __launch_bounds__(64 * NW, 1) void scan_screen_kernel(const int8_t* _
       }
     }
   };
+  // the quantiser's seed bound for the lane's query (k_screen.hip kSeedRows: a lower bound of a_k, 0 = none),
+  // in the words after the XCD split's
+  if (xb != nullptr) {
+    thr = xb[kXbWords + q];
+    set_bounds();
+  }
   // MODE 32 (debug) counts slow-path entries in slot 15 of each wave's first query: 15 slots then;
   // MODE 256 (debug): kernel 6's bound, the min over KL slots (list j -> slot j % KL)
   constexpr int kSlots = (MODE & 256) != 0 ? KL : (MODE & 32) != 0 ? kTauW - 1 : kTauW;

@@ -236,6 +236,10 @@ __global__ __launch_bounds__(256, 1) void scan_screen_q64_kernel(const int8_t* _
 #pragma unroll
     for (int qb = 0; qb < 4; ++qb) tfq[qb] = __shfl(tf_own, 16 * qb + (lane & 15));
   };
+  if (xb != nullptr) {  // the quantiser's seed bound (kernel 10)
+    thr = xb[kXbWords + q];
+    set_bounds();
+  }
   const uint32_t slot_voff = (uint32_t)(q * kTauW + lst % kTauW) * 4u;
   const uint8_t* const tq = lds + kTauOff + (w * kQW + lane) * (kTauW * 4);
   const uint8_t* const frag_base = lds + (lane & 15) * kRowB;

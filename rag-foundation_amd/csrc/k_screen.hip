@@ -168,13 +168,24 @@ __global__ __launch_bounds__(256) void screen_quantize_kernel(const void* __rest
 // their tiles per XCD, summed by kernel 10 since the last query quantiser.
 __device__ uint32_t g_xcd_w[24];
 
+// The seed (round 6): kernel 10's blocks start with no bound, so their first tiles pass nearly every value
+// (16 slow-path trips per wave at tiles 0 and 1: a third of all trips at the 8-GPU shard).  The
+// quantiser gives each query a bound to start from: the KL-th best screen score A = fl(D s_t) over kSeedRows
+// live, allowed sample rows spread over the store (rows i * rows / S).  They are distinct live rows, so the
+// KL-th best of their A is at most the KL-th best over all live rows, hence at most a_k (KL >= k): a valid
+// lower bound, like the slot table's.  No seed (0) with fewer than KL such rows.
+constexpr int kSeedRows = 256;
+
 template <int DT, int D>
 __global__ __launch_bounds__(256) void screen_queries_kernel(const void* __restrict__ Q, int nq, int nq_pad,
                                                              int8_t* __restrict__ Qc, float* __restrict__ qe2,
                                                              const uint32_t* __restrict__ stats,
                                                              uint32_t* __restrict__ tau, uint32_t* __restrict__ gate,
                                                              uint32_t* __restrict__ ftau, int ftau_nq,
-                                                             uint32_t* __restrict__ xb) {
+                                                             uint32_t* __restrict__ xb, const int8_t* __restrict__ X8,
+                                                             const uint4* __restrict__ tmeta, int nrows,
+                                                             const uint32_t* __restrict__ mask, int kl,
+                                                             uint32_t* __restrict__ seed) {
   constexpr int NM = D / 256;
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -240,6 +251,7 @@ __global__ __launch_bounds__(256) void screen_queries_kernel(const void* __restr
   const float s = am > 0.f ? __fdiv_rn(am, 127.f) : 0.f;
   double ey = 0.0;
   int cc = 0;  // <= D 127^2 < 2^31
+  uint32_t pkm[NM];  // (the seed below reads them back)
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
     uint32_t pk = 0u;
@@ -252,9 +264,80 @@ __global__ __launch_bounds__(256) void screen_queries_kernel(const void* __restr
       cc += (int)c * c;
     }
     *(uint32_t*)(Qc + (int64_t)q * D + 256 * m + 4 * lane) = pk;
+    pkm[m] = pk;
   }
   ey = wave_sum_f64(ey);
   cc = wave_sum_i32(cc);
+  if (seed) {
+    // the seed: 16 lanes per sample row (lane gl holds 16-B chunks gl + 16 u of the row and of the query codes,
+    // gathered from the lanes that hold them: lane l has bytes 256 m + 4 l .. + 3), 4 rows per group in flight
+    constexpr int NU = D / 256;
+    __shared__ float sv[4][kSeedRows];
+    const int wv = threadIdx.x >> 6, g = lane >> 4, gl = lane & 15;
+    uint4 qd[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      qd[u].x = __shfl(pkm[u], 4 * gl + 0);
+      qd[u].y = __shfl(pkm[u], 4 * gl + 1);
+      qd[u].z = __shfl(pkm[u], 4 * gl + 2);
+      qd[u].w = __shfl(pkm[u], 4 * gl + 3);
+    }
+    const int S = nrows < kSeedRows ? nrows : kSeedRows;
+    for (int i0 = 0; i0 < S; i0 += 16) {
+      uint4 xv[4][NU];
+      int rr[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int i = i0 + 4 * g + t;
+        rr[t] = (int)((int64_t)(i < S ? i : 0) * nrows / S);
+#pragma unroll
+        for (int u = 0; u < NU; ++u) xv[t][u] = *(const uint4*)(X8 + (int64_t)rr[t] * D + 16 * (gl + 16 * u));
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        int acc = 0;
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          acc = __builtin_amdgcn_sdot4((int)xv[t][u].x, (int)qd[u].x, acc, false);
+          acc = __builtin_amdgcn_sdot4((int)xv[t][u].y, (int)qd[u].y, acc, false);
+          acc = __builtin_amdgcn_sdot4((int)xv[t][u].z, (int)qd[u].z, acc, false);
+          acc = __builtin_amdgcn_sdot4((int)xv[t][u].w, (int)qd[u].w, acc, false);
+        }
+        const float dsum = row16_sum((float)acc);  // |partial sums| < 2^24: exact in f32
+        const int i = i0 + 4 * g + t;
+        if (gl == 0 && i < S) {
+          const uint4 md = tmeta[rr[t] >> 5];
+          const int r = rr[t];
+          const bool ok = ((md.y >> (r & 31)) & 1u) && (mask == nullptr || ((mask[r >> 5] >> (r & 31)) & 1u));
+          sv[wv][i] = ok ? dsum * __uint_as_float(md.x) : -__builtin_inff();  // A = s_t D, one rounding
+        }
+      }
+    }
+    // the KL-th best of the S values (4 per lane, sorted; kl rounds of a wave max)
+    float a[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] = 64 * j + lane < S ? sv[wv][64 * j + lane] : -__builtin_inff();
+    auto cx = [](float& x, float& y) {
+      const float hi = fmaxf(x, y), lo = fminf(x, y);
+      x = hi;
+      y = lo;
+    };
+    cx(a[0], a[1]);
+    cx(a[2], a[3]);
+    cx(a[0], a[2]);
+    cx(a[1], a[3]);
+    cx(a[1], a[2]);
+    float mx = -__builtin_inff();
+    for (int it = 0; it < kl; ++it) {
+      mx = wave_max_f32(a[0]);
+      const bool win = lane == (int)__builtin_ctzll(__ballot(a[0] == mx));
+      a[0] = win ? a[1] : a[0];
+      a[1] = win ? a[2] : a[1];
+      a[2] = win ? a[3] : a[2];
+      a[3] = win ? -__builtin_inff() : a[3];
+    }
+    if (lane == 0) seed[q] = (q < nq && mx > -__builtin_inff()) ? ord(mx) : 0u;
+  }
   if (lane == 0) {
     float e2 = 0.f;
     if (s > 0.f) {
@@ -558,9 +641,9 @@ MfmaPlan plan_scan_screen(int64_t nrows, int D, int dtype, int64_t nq, int k, in
   return p;
 }
 
-// the slot table [nq_pad][16], then kernel 10's XCD-split words (k10::kXbWords)
+// the slot table [nq_pad][16], then kernel 10's XCD-split words (k10::kXbWords), then the seeds [nq_pad]
 size_t tau_bytes_screen(const MfmaPlan& p) {
-  return ((size_t)p.nq_pad * k10::kTauW + k10::kXbWords) * sizeof(uint32_t);
+  return ((size_t)p.nq_pad * k10::kTauW + k10::kXbWords + (size_t)p.nq_pad) * sizeof(uint32_t);
 }
 
 uint32_t* xcd_weights_device_ptr() {
@@ -573,12 +656,22 @@ uint32_t* xcd_weights_device_ptr() {
 
 void launch_screen_queries(const void* Q, int dtype, int D, int64_t nq, int64_t nq_pad, int8_t* Qc, float* qe2,
                            const uint32_t* stats, uint32_t* tau, uint32_t* gate, uint32_t* ftau, int64_t ftau_nq,
-                           hipStream_t st) {
+                           hipStream_t st, const ScreenSeed* sd) {
   if (!ftau) ftau_nq = 0;
   const dim3 grid((unsigned)((std::max(nq_pad, ftau_nq) + 3) / 4));
+  // the seed words follow the slot table and the XCD words (tau_bytes_screen); RFX_K10_SEED=0: none (A/B)
+  static const bool seed_on = [] {
+    const char* e = getenv("RFX_K10_SEED");
+    return !(e && e[0] == '0');
+  }();
+  uint32_t* seed = tau + nq_pad * k10::kTauW + k10::kXbWords;
+  const bool use = sd && sd->X8 && sd->nrows > 0 && seed_on;
+  if (!use) (void)hipMemsetAsync(seed, 0, (size_t)nq_pad * 4, st);  // (no seed: kernel 10 reads zeros)
 #define RFX_SQQ(DTV, DV)                                                                                       \
   hipLaunchKernelGGL((screen_queries_kernel<DTV, DV>), grid, dim3(256), 0, st, Q, (int)nq, (int)nq_pad, Qc, qe2,  \
-                     stats, tau, gate, ftau, (int)ftau_nq, tau + nq_pad * k10::kTauW)
+                     stats, tau, gate, ftau, (int)ftau_nq, tau + nq_pad * k10::kTauW, use ? sd->X8 : nullptr,      \
+                     use ? (const uint4*)sd->tmeta : nullptr, use ? sd->nrows : 0, use ? sd->mask : nullptr,       \
+                     use ? sd->kl : 0, use ? seed : nullptr)
   if (dtype == RFX_BF16 && D == 768)
     RFX_SQQ(RFX_BF16, 768);
   else if (dtype == RFX_BF16)

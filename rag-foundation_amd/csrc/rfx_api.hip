@@ -647,8 +647,14 @@ int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t
   uint32_t* tau = (uint32_t*)(ws + L.tau_off);
   // the fallback's threshold table ([its nq_pad][16]) is zeroed by the query quantiser: no memset launch
   if (stages & 1) {
+    rfx::ScreenSeed sd;
+    sd.X8 = ix.scodes;
+    sd.tmeta = ix.smeta;
+    sd.nrows = (int)ix.rows;
+    sd.mask = mask;
+    sd.kl = L.sp.k_lane;
     rfx::launch_screen_queries(queries, ix.dtype, ix.dim, nq, L.sp.nq_pad, qc, qe2, ix.sstats, stau, gate, tau,
-                               L.mp.nq_pad, st);
+                               L.mp.nq_pad, st, &sd);
     if (ev0) RFX_HIP(hipEventRecord((hipEvent_t)ev0, st));
     if (rfx::launch_scan_screen(L.sp, ix.scodes, ix.smeta, ix.sstats, (int)ix.rows, ix.dim, qc, qe2, (int)nq, stau, scs,
                                 scr, drops, st, mask) != 0)
@@ -1502,8 +1508,13 @@ int rfx_dbg_screen_variant(rfx_index_t h, const void* queries_d, int64_t nq, int
   int8_t* qc = (int8_t*)(ws + L.s_qc);
   float* qe2 = (float*)(ws + L.s_qe2);
   uint32_t* stau = (uint32_t*)(ws + L.s_tau);
+  rfx::ScreenSeed sd;
+  sd.X8 = ix->scodes;
+  sd.tmeta = ix->smeta;
+  sd.nrows = (int)ix->rows;
+  sd.kl = L.sp.k_lane;
   rfx::launch_screen_queries(queries_d, ix->dtype, ix->dim, nq, L.sp.nq_pad, qc, qe2, ix->sstats, stau,
-                             (uint32_t*)(ws + L.s_gate), nullptr, 0, st);
+                             (uint32_t*)(ws + L.s_gate), nullptr, 0, st, &sd);
   // RFX_DBG_KEEP_TAU=1: the slot table starts from the previous launch's final one (the same queries on
   // the same rows: still a lower bound of a_k) — the timing of a bound with no warm-up at all
   static const bool keep_tau = getenv("RFX_DBG_KEEP_TAU") != nullptr;
@@ -1544,7 +1555,13 @@ int rfx_dbg_screen_search(rfx_index_t h, const void* queries_d, int64_t nq, int 
   float* qe2 = (float*)(ws + L.s_qe2);
   uint32_t* stau = (uint32_t*)(ws + L.s_tau);
   uint32_t* gate = (uint32_t*)(ws + L.s_gate);
-  rfx::launch_screen_queries(queries_d, ix->dtype, ix->dim, nq, L.sp.nq_pad, qc, qe2, ix->sstats, stau, gate, nullptr, 0, st);
+  rfx::ScreenSeed sd;
+  sd.X8 = ix->scodes;
+  sd.tmeta = ix->smeta;
+  sd.nrows = (int)ix->rows;
+  sd.kl = L.sp.k_lane;
+  rfx::launch_screen_queries(queries_d, ix->dtype, ix->dim, nq, L.sp.nq_pad, qc, qe2, ix->sstats, stau, gate, nullptr, 0,
+                             st, &sd);
   if (rfx::launch_scan_screen_dbg(L.sp, variant, ix->scodes, ix->smeta, ix->sstats, (int)ix->rows, qc, qe2, (int)nq, stau,
                                   (float*)(ws + L.s_cs), (int*)(ws + L.s_cr), (uint32_t*)(ws + L.s_drop), st) != 0)
     return fail(RFX_EUNSUPPORTED, "screen variant %d unsupported", variant);

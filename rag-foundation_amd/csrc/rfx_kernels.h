@@ -147,10 +147,19 @@ uint32_t* xcd_weights_device_ptr();  // kernel 10's per-device XCD weight table 
 // ftau (or null): the gated fallback scan's threshold table ([nq_pad][kFallbackTauW], kernel 6 / 8),
 // zeroed here so the fallback launch needs no memset of its own (tau_zeroed below)
 constexpr int kFallbackTauW = 16;
-// ftau_nq: the fallback's padded batch (its table rows zeroed; may exceed nq_pad)
+// ftau_nq: the fallback's padded batch (its table rows zeroed; may exceed nq_pad).  sd (kernel 10's plans):
+// the int8 copy, its rows, the row mask and the lane-list length, from which each query's seed bound is taken
+// (k_screen.hip); nullptr: the seed words are zeroed (no seed)
+struct ScreenSeed {
+  const int8_t* X8 = nullptr;
+  const void* tmeta = nullptr;
+  int nrows = 0;
+  const uint32_t* mask = nullptr;
+  int kl = 0;
+};
 void launch_screen_queries(const void* Q, int dtype, int D, int64_t nq, int64_t nq_pad, int8_t* Qc, float* qe2,
                            const uint32_t* stats, uint32_t* tau, uint32_t* gate, uint32_t* ftau, int64_t ftau_nq,
-                           hipStream_t st);
+                           hipStream_t st, const ScreenSeed* sd = nullptr);
 int launch_scan_screen(const MfmaPlan& p, const int8_t* codes, const void* tmeta, const uint32_t* stats, int nrows, int D,
                        const int8_t* Qc, const float* qe2, int nq, uint32_t* tau, float* cs, int* cr, uint32_t* drops,
                        hipStream_t st, const uint32_t* mask);
