@@ -268,7 +268,9 @@ __global__ __launch_bounds__(256) void screen_queries_kernel(const void* __restr
   }
   ey = wave_sum_f64(ey);
   cc = wave_sum_i32(cc);
-  if (seed) {
+  if (seed && (X8 == nullptr || kl <= 0)) {
+    if (lane == 0) seed[q] = 0u;  // (no seed: kernel 10 starts with no bound)
+  } else if (seed) {
     // the seed: 16 lanes per sample row (lane gl holds 16-B chunks gl + 16 u of the row and of the query codes,
     // gathered from the lanes that hold them: lane l has bytes 256 m + 4 l .. + 3), 4 rows per group in flight
     constexpr int NU = D / 256;
@@ -659,19 +661,19 @@ void launch_screen_queries(const void* Q, int dtype, int D, int64_t nq, int64_t 
                            hipStream_t st, const ScreenSeed* sd) {
   if (!ftau) ftau_nq = 0;
   const dim3 grid((unsigned)((std::max(nq_pad, ftau_nq) + 3) / 4));
-  // the seed words follow the slot table and the XCD words (tau_bytes_screen); RFX_K10_SEED=0: none (A/B)
+  // the seed words follow the slot table and the XCD words (tau_bytes_screen).  Off by default: measured
+  // no faster; RFX_K10_SEED=1 computes it (A/B), otherwise the quantiser writes zeros.
   static const bool seed_on = [] {
     const char* e = getenv("RFX_K10_SEED");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   uint32_t* seed = tau + nq_pad * k10::kTauW + k10::kXbWords;
   const bool use = sd && sd->X8 && sd->nrows > 0 && seed_on;
-  if (!use) (void)hipMemsetAsync(seed, 0, (size_t)nq_pad * 4, st);  // (no seed: kernel 10 reads zeros)
 #define RFX_SQQ(DTV, DV)                                                                                       \
   hipLaunchKernelGGL((screen_queries_kernel<DTV, DV>), grid, dim3(256), 0, st, Q, (int)nq, (int)nq_pad, Qc, qe2,  \
                      stats, tau, gate, ftau, (int)ftau_nq, tau + nq_pad * k10::kTauW, use ? sd->X8 : nullptr,      \
                      use ? (const uint4*)sd->tmeta : nullptr, use ? sd->nrows : 0, use ? sd->mask : nullptr,       \
-                     use ? sd->kl : 0, use ? seed : nullptr)
+                     use ? sd->kl : 0, seed)
   if (dtype == RFX_BF16 && D == 768)
     RFX_SQQ(RFX_BF16, 768);
   else if (dtype == RFX_BF16)
