@@ -133,31 +133,29 @@ __device__ __forceinline__ void fold_first(const Acc4View& acc, uint64_t* Ls, ui
 // 256 = tile 0 folded by rank (fold_first), 512 = MFMAs of a k-step in snake order.
 constexpr int kModeMask = 2097152;
 
+// The body of one workgroup: row range `range` of `nblk`, query group `qgb`, in the LDS image `lds`
+// (lds_bytes<KL, RING>() bytes, 1024-aligned).  scan_mfma6_kernel runs it as block (range, qgb) of its
+// grid; the two-pass select with the fallback inside its launch (k_select_fb.h) as a claimed unit.
 template <int DT, int KL, int D, int MODE = 0, int RING = kRing>
-__global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Qp,
-                                                            int nq, int ntiles, uint32_t* __restrict__ tau,
-                                                            float* __restrict__ cand_s, int* __restrict__ cand_r,
-                                                            int64_t n_lists, const uint32_t* __restrict__ mask,
-                                                            const uint32_t* __restrict__ gate) {
-  // gate (the two-pass scan's fallback, k_screen.hip): run only when the screen asked for it
-  if (gate && *gate == 0u) return;
+__device__ __forceinline__ void scan_mfma6_body(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Qp, int nq,
+                                                int ntiles, uint32_t* __restrict__ tau, float* __restrict__ cand_s,
+                                                int* __restrict__ cand_r, int64_t n_lists,
+                                                const uint32_t* __restrict__ mask, int range, int qgb, int nblk,
+                                                uint8_t* __restrict__ lds) {
   constexpr int NKS = D / 32;   // 32-deep k-steps per tile
   constexpr int NST = D / kSK;  // stages per tile
   constexpr int KPS = kSK / 32;  // k-steps per stage (8)
   static_assert(D % kSK == 0, "D must be a multiple of 256");
   static_assert(KL <= 10, "threshold table holds 10 slots");
-  __shared__ __attribute__((aligned(1024))) uint8_t lds[lds_bytes<KL, RING>()];
   constexpr int kTauOff = tau_off<RING>();
   constexpr int kListOff = list_off<RING>();
 
   const int tid = threadIdx.x;
   const int w = tid >> 6, lane = tid & 63;
   const int half = lane >> 5;
-  const int range = blockIdx.x;
-  const int qg = blockIdx.y * kQG;
+  const int qg = qgb * kQG;
   // this lane's query after the epilogue's pair swap: lanes of odd 16-lane row hold query block 1
   const int q = qg + w * kQW + 16 * ((lane >> 4) & 1) + (lane & 15);
-  const int nblk = gridDim.x;
   const int nt = range < ntiles ? (ntiles - range + nblk - 1) / nblk : 0;
   const int S = nt * NST;
   if (S == 0) return;  // (cannot happen with the host plan; whole workgroup exits together)
@@ -382,6 +380,19 @@ __global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __re
       cand_r[o + i] = keep ? (int)(~(uint32_t)key) : kEmptyRow;
     }
   }
+}
+
+template <int DT, int KL, int D, int MODE = 0, int RING = kRing>
+__global__ __launch_bounds__(512, 1) void scan_mfma6_kernel(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Qp,
+                                                            int nq, int ntiles, uint32_t* __restrict__ tau,
+                                                            float* __restrict__ cand_s, int* __restrict__ cand_r,
+                                                            int64_t n_lists, const uint32_t* __restrict__ mask,
+                                                            const uint32_t* __restrict__ gate) {
+  // gate (the two-pass scan's fallback, k_screen.hip): run only when the screen asked for it
+  if (gate && *gate == 0u) return;
+  __shared__ __attribute__((aligned(1024))) uint8_t lds[lds_bytes<KL, RING>()];
+  scan_mfma6_body<DT, KL, D, MODE, RING>(X, Qp, nq, ntiles, tau, cand_s, cand_r, n_lists, mask, (int)blockIdx.x,
+                                         (int)blockIdx.y, (int)gridDim.x, lds);
 }
 
 // one translation unit per (dtype, D) instantiates the kernel for the lane-list sizes KL in {4, 10}

@@ -7,6 +7,18 @@
 // oracle/screen.py restates every step; the codes, tile scales and live words are bit-exact with it
 // (one correctly rounded IEEE op per float step: __fdiv_rn, rintf).
 #include "k_scan_screen.h"
+#ifdef RFX_DEBUG_BUILD
+namespace rfx {
+namespace {
+// debug library only: per block (query < 256) the 100-MHz wall clock at the select's phase ends
+// (tools/select_phases.py via rfx_dbg_select_times)
+__device__ unsigned long long g_sel_t[256][8];
+}  // namespace
+}  // namespace rfx
+#define RFX_SEL_T(i) \
+  if (threadIdx.x == 0 && blockIdx.x < 256) ::rfx::g_sel_t[blockIdx.x][i] = wall_clock64();
+#endif
+#include "k_select.h"
 
 namespace rfx {
 namespace k10 {
@@ -28,12 +40,6 @@ namespace {
 
 using mfc::ord;
 using mfc::unord;
-
-struct Rec {  // the merge records of rfx/dist.py pack(): {f32 score, i32 pad, i64 row}
-  float s;
-  int pad;
-  long long r;
-};
 
 template <int DT>
 __device__ __forceinline__ float widen(uint16_t h) {
@@ -189,7 +195,7 @@ __global__ __launch_bounds__(256) void screen_queries_kernel(const void* __restr
   constexpr int NM = D / 256;
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *gate = 0u;
+  if (blockIdx.x == 0 && threadIdx.x < 64) gate[threadIdx.x] = 0u;  // the gate and the select's control words
   if (blockIdx.x == 0 && threadIdx.x < 64) {
     // Kernel 10's split for this launch (lanes 0..7 = XCDs): the speed each XCD measured since the last
     // quantiser (tiles per tick, the sums taken and reset), its weight moved half-way to its share of
@@ -352,39 +358,7 @@ __global__ __launch_bounds__(256) void screen_queries_kernel(const void* __restr
   }
 }
 
-// ---- select: survivors, exact re-score, top-k (one 512-thread block per query) --------------------
-constexpr int kSelCap = 2048;  // kept candidates per query held in LDS; more -> fallback (8 waves x 256)
-constexpr int kSelK = 16;      // k <= kSelK (kernel 10 plans k <= 10)
-
-#ifdef RFX_DEBUG_BUILD
-// debug library only: per block (query < 256) the 100-MHz wall clock at the select's phase ends
-// (tools/select_phases.py via rfx_dbg_select_times)
-__device__ unsigned long long g_sel_t[256][8];
-#define RFX_SEL_T(i)                                  \
-  if (threadIdx.x == 0 && blockIdx.x < 256) g_sel_t[blockIdx.x][i] = wall_clock64();
-#else
-#define RFX_SEL_T(i)
-#endif
-
-// one 16-B chunk's products added to acc in f64 (f32 products of bf16 / f16 values are exact; f32 values are
-// multiplied in f64, also exact)
-template <int DT>
-__device__ __forceinline__ void chunk_dot(double& acc, const uint4& x, const uint4& y) {
-  const uint32_t xx[4] = {x.x, x.y, x.z, x.w};
-  const uint32_t yy[4] = {y.x, y.y, y.z, y.w};
-  if constexpr (DT == RFX_F32) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) acc += (double)__uint_as_float(xx[e]) * (double)__uint_as_float(yy[e]);
-  } else {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const uint16_t xh = (uint16_t)(e & 1 ? xx[e >> 1] >> 16 : xx[e >> 1] & 0xffffu);
-      const uint16_t yh = (uint16_t)(e & 1 ? yy[e >> 1] >> 16 : yy[e >> 1] & 0xffffu);
-      acc += (double)(widen<DT>(xh) * widen<DT>(yh));
-    }
-  }
-}
-
+// ---- select: survivors, exact re-score, top-k (one 512-thread block per query; k_select.h) ----------
 template <int DT, int D>
 __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restrict__ cs, const int* __restrict__ cr,
                                                             const uint32_t* __restrict__ drops, int64_t n_lists,
@@ -392,167 +366,11 @@ __global__ __launch_bounds__(512) void screen_select_kernel(const float* __restr
                                                             const uint8_t* __restrict__ Q,
                                                             const uint8_t* __restrict__ X, int k, int64_t row_offset,
                                                             float* __restrict__ out_s, int64_t* __restrict__ out_r,
-                                                            Rec* __restrict__ out_rec, uint32_t* __restrict__ gate,
+                                                            sel::Rec* __restrict__ out_rec, uint32_t* __restrict__ gate,
                                                             int* __restrict__ diag, int force) {
-  // U1: candidate entries per thread per round (config 3: 512 lists x 10 = 5,120 = one round, rows
-  // loaded with the scores, and the drops with them: one memory round trip instead of four).
-  // The exact re-score: 16 lanes per survivor row (CPL 16-B chunks of the row per lane), U rows per
-  // 16-lane group in flight: 8 waves x 4 groups x U = 96 rows per round (config 3: 94 survivors on
-  // average, so one round, one memory latency)
-  // rows and queries are read as 16-B chunks: chunk c of a row holds its bytes [16 c, 16 c + 16) (8 bf16 / f16
-  // or 4 f32 elements); lane gl of a 16-lane group takes chunks gl + 16 i, i < CPL
-  constexpr int RB = D * (DT == RFX_F32 ? 4 : 2);
-  constexpr int NT = 512, NW = NT / 64, CPL = RB / 256, U = DT == RFX_F32 ? 2 : 3, U1 = 10, RPR = NW * 4 * U;
-  __shared__ __attribute__((aligned(16))) float ca[kSelCap];  // screen score A of kept candidate i
-  __shared__ int crow[kSelCap];   // its row
-  __shared__ int srow[kSelCap];   // survivor j's row
-  // survivor j's rank key: (orderable fl32 of the exact f64 sum) << 32 | ~row — larger key = better
-  // under (score desc, row asc), so a rank is one 64-bit compare per survivor, no branches
-  __shared__ uint64_t skey[kSelCap];
-  __shared__ uint64_t res_key[64];  // the answer, written out by one wave
-  __shared__ int n_c, n_sv, fail;
-  __shared__ float ak;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const int64_t q = blockIdx.x;
-  RFX_SEL_T(0)
-  if (tid == 0) {
-    n_c = n_sv = fail = 0;
-    ak = -__builtin_inff();
-  }
-  // the query's row chunks for the re-score (16-lane layout below), loaded with everything else
-  const int gl = lane & 15, grp = w * 4 + (lane >> 4);
-  uint4 yq[CPL];
-#pragma unroll
-  for (int c = 0; c < CPL; ++c) yq[c] = *(const uint4*)(Q + q * RB + (gl + 16 * c) * 16);
-  __syncthreads();
-  // 1. compact the kept candidates (the scan wrote -inf for empty slots and dropped entries)
-  const int64_t n = n_lists * list_len;
-  const float* qs = cs + q * n;
-  const int* qr = cr + q * n;
-  const uint32_t d0 = tid < n_lists ? drops[q * n_lists + tid] : 0u;  // step 3's, loaded now
-  for (int64_t b = tid; b < n; b += (int64_t)NT * U1) {
-    float s[U1];
-    int r[U1];
-#pragma unroll
-    for (int u = 0; u < U1; ++u) {
-      const bool in = b + u * NT < n;
-      s[u] = in ? qs[b + u * NT] : -__builtin_inff();
-      r[u] = in ? qr[b + u * NT] : 0;
-    }
-#pragma unroll
-    for (int u = 0; u < U1; ++u)
-      if (s[u] != -__builtin_inff()) {
-        const int i = atomicAdd(&n_c, 1);
-        if (i < kSelCap) {
-          ca[i] = s[u];
-          crow[i] = r[u];
-        }
-      }
-  }
-  __syncthreads();
-  RFX_SEL_T(1)
-  const int nc = n_c;
-  if (nc > kSelCap || force) fail = 1;
-  const int ncl = nc < kSelCap ? nc : kSelCap;
-  // 2. a_k = the k-th best A (with multiplicity): the value v with #{> v} < k <= #{>= v}.  Every
-  // candidate counts the others with 16-B broadcast reads (4 per read; the tail padded with -inf,
-  // which counts for nothing).  Measured faster than extracting each wave's k best by k rounds of a
-  // DPP wave max (1.96 against 4.72 us at the 8-GPU shard, ~108 candidates per query: those rounds
-  // are a serial dependency chain).
-  if (tid < 3 && ncl + tid < kSelCap) ca[ncl + tid] = -__builtin_inff();
-  __syncthreads();
-  {
-    const float4* ca4 = (const float4*)ca;
-    const int n4 = (ncl + 3) >> 2;
-    for (int i = tid; i < ncl; i += NT) {
-      const float si = ca[i];
-      int gt = 0, ge = 0;
-#pragma unroll 8
-      for (int j = 0; j < n4; ++j) {
-        const float4 v = ca4[j];
-        gt += (v.x > si) + (v.y > si) + (v.z > si) + (v.w > si);
-        ge += (v.x >= si) + (v.y >= si) + (v.z >= si) + (v.w >= si);
-      }
-      if (gt < k && ge >= k) ak = si;  // every writer writes the same value
-    }
-  }
-  __syncthreads();
-  RFX_SEL_T(2)
-  const float e2 = qe2[q];
-  const float t = ncl >= k ? ak - e2 : -__builtin_inff();
-  const uint32_t ot = ord(t);
-  // 3. a row dropped at or above t could be a survivor the lists lost: fallback
-  if (d0 && d0 >= ot) fail = 1;
-  for (int64_t j = tid + NT; j < n_lists; j += NT) {
-    const uint32_t d = drops[q * n_lists + j];
-    if (d && d >= ot) fail = 1;
-  }
-  for (int i = tid; i < ncl; i += NT)
-    if (ca[i] >= t) srow[atomicAdd(&n_sv, 1)] = crow[i];
-  __syncthreads();
-  RFX_SEL_T(3)
-  if (fail) {
-    if (tid == 0) __hip_atomic_store(gate, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (diag && tid == 0) {
-      diag[q * 2] = nc;
-      diag[q * 2 + 1] = -1;
-    }
-    return;  // the gated exact pass rewrites the whole batch
-  }
-  const int ns = n_sv;
-  // 4. exact re-score: the 16 lanes of a group hold chunks gl + 16 c of the row (8 elements each); f32
-  // products of bf16 / f16 values are exact, their sum is taken in f64 (the oracle's f64 dot up to
-  // f64 rounding), rounded once to f32
-  for (int j0 = grp; j0 < ns; j0 += RPR) {
-    uint4 xv[U][CPL];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = j0 + u * NW * 4;
-      const int64_t row = j < ns ? (int64_t)srow[j] : (int64_t)srow[0];
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) xv[u][c] = *(const uint4*)(X + row * RB + (gl + 16 * c) * 16);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      double acc = 0.0;
-#pragma unroll
-      for (int c = 0; c < CPL; ++c) chunk_dot<DT>(acc, xv[u][c], yq[c]);
-      acc = row16_sum_f64(acc);  // within the 16-lane group (DPP; lane 0's sum = the xor butterfly's)
-      const int j = j0 + u * NW * 4;
-      if (gl == 0 && j < ns) skey[j] = ((uint64_t)ord((float)acc) << 32) | (uint32_t)(~(uint32_t)srow[j]);
-    }
-  }
-  __syncthreads();
-  RFX_SEL_T(4)
-  // 5. top-k of the survivors by (exact score desc, row asc) with the exact score rounded to f32 first
-  // (the order every merge of f32 scores keeps: a sharded store's gathered merge, kernel 11); NaN
-  // (cannot occur for live rows) last.  The k best land in LDS; one wave writes them out.
-  for (int j = tid; j < ns; j += NT) {
-    const uint64_t kj = skey[j];
-    int rank = 0;
-#pragma unroll 8
-    for (int i = 0; i < ns; ++i) rank += skey[i] > kj ? 1 : 0;
-    if (rank < k) res_key[rank] = kj;
-  }
-  RFX_SEL_T(6)
-  __syncthreads();
-  if (tid < k) {
-    const bool ok = tid < ns;  // (survivors are live rows: never NaN)
-    const uint64_t kk = ok ? res_key[tid] : 0ull;
-    const float sf = ok ? unord((uint32_t)(kk >> 32)) : -__builtin_inff();
-    const long long rr = ok ? (long long)(int)(~(uint32_t)kk) + row_offset : -1;
-    if (out_rec) {
-      out_rec[q * k + tid] = Rec{sf, 0, rr};
-    } else {
-      out_s[q * k + tid] = sf;
-      out_r[q * k + tid] = rr;
-    }
-  }
-  if (diag && tid == 0) {
-    diag[q * 2] = nc;
-    diag[q * 2 + 1] = ns;
-  }
-  RFX_SEL_T(5)
+  __shared__ sel::SelLds sl;
+  sel::select_body<DT, D>(cs, cr, drops, n_lists, list_len, qe2, Q, X, k, row_offset, out_s, out_r, out_rec, gate, diag,
+                          force, (int64_t)blockIdx.x, sl);
 }
 
 }  // namespace
@@ -707,11 +525,11 @@ int launch_screen_select(const float* cs, const int* cr, const uint32_t* drops, 
                          int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec, uint32_t* gate, int* diag,
                          int force, hipStream_t st) {
   if (nq <= 0) return 0;
-  if (k < 1 || k > kSelK) return -1;
+  if (k < 1 || k > sel::kSelK) return -1;
 #define RFX_SEL(DTV, DV)                                                                                          \
   hipLaunchKernelGGL((screen_select_kernel<DTV, DV>), dim3((unsigned)nq), dim3(512), 0, st, cs, cr, drops, n_lists, \
                      list_len, qe2, (const uint8_t*)Q, (const uint8_t*)X, k, row_offset, out_s, out_r,             \
-                     (Rec*)out_rec, gate, diag, force)
+                     (sel::Rec*)out_rec, gate, diag, force)
   if (dtype == RFX_BF16 && D == 768)
     RFX_SEL(RFX_BF16, 768);
   else if (dtype == RFX_BF16)
@@ -726,6 +544,29 @@ int launch_screen_select(const float* cs, const int* cr, const uint32_t* drops, 
     RFX_SEL(RFX_F16, 1024);
 #undef RFX_SEL
   return 0;
+}
+
+namespace selfb {
+int launch_bf16_768(const SelectFb& a, hipStream_t st);
+int launch_f16_768(const SelectFb& a, hipStream_t st);
+}  // namespace selfb
+
+// RFX_SELECT_FB=0 (A/B): the select, the gated kernel-6 scan and the gated merge as three launches
+bool select_fb_supported(int D, int dtype) {
+  static const bool on = [] {
+    const char* e = getenv("RFX_SELECT_FB");
+    return !(e && e[0] == '0');
+  }();
+  return on && D == 768 && (dtype == RFX_BF16 || dtype == RFX_F16);
+}
+
+int launch_screen_select_fb(const SelectFb& a, int D, int dtype, hipStream_t st) {
+  if (a.nq <= 0) return 0;
+  if (a.k < 1 || a.k > sel::kSelK || a.k > a.mp.k_lane || !a.diag || !a.ctl || !a.mp.ok) return -1;
+  if (D != 768 || a.nq > a.mp.nq_pad) return -1;
+  if (dtype == RFX_BF16) return selfb::launch_bf16_768(a, st);
+  if (dtype == RFX_F16) return selfb::launch_f16_768(a, st);
+  return -1;
 }
 
 }  // namespace rfx
