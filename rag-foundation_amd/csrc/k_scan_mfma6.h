@@ -134,8 +134,7 @@ __device__ __forceinline__ void fold_first(const Acc4View& acc, uint64_t* Ls, ui
 constexpr int kModeMask = 2097152;
 
 // The body of one workgroup: row range `range` of `nblk`, query group `qgb`, in the LDS image `lds`
-// (lds_bytes<KL, RING>() bytes, 1024-aligned).  scan_mfma6_kernel runs it as block (range, qgb) of its
-// grid; the two-pass select with the fallback inside its launch (k_select_fb.h) as a claimed unit.
+// (lds_bytes<KL, RING>() bytes, 1024-aligned); scan_mfma6_kernel runs it as block (range, qgb) of its grid.
 template <int DT, int KL, int D, int MODE = 0, int RING = kRing>
 __device__ __forceinline__ void scan_mfma6_body(const uint16_t* __restrict__ X, const uint16_t* __restrict__ Qp, int nq,
                                                 int ntiles, uint32_t* __restrict__ tau, float* __restrict__ cand_s,

@@ -195,7 +195,7 @@ __global__ __launch_bounds__(256) void screen_queries_kernel(const void* __restr
   constexpr int NM = D / 256;
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (blockIdx.x == 0 && threadIdx.x < 64) gate[threadIdx.x] = 0u;  // the gate and the select's control words
+  if (blockIdx.x == 0 && threadIdx.x == 0) *gate = 0u;
   if (blockIdx.x == 0 && threadIdx.x < 64) {
     // Kernel 10's split for this launch (lanes 0..7 = XCDs): the speed each XCD measured since the last
     // quantiser (tiles per tick, the sums taken and reset), its weight moved half-way to its share of
@@ -544,29 +544,6 @@ int launch_screen_select(const float* cs, const int* cr, const uint32_t* drops, 
     RFX_SEL(RFX_F16, 1024);
 #undef RFX_SEL
   return 0;
-}
-
-namespace selfb {
-int launch_bf16_768(const SelectFb& a, hipStream_t st);
-int launch_f16_768(const SelectFb& a, hipStream_t st);
-}  // namespace selfb
-
-// RFX_SELECT_FB=0 (A/B): the select, the gated kernel-6 scan and the gated merge as three launches
-bool select_fb_supported(int D, int dtype) {
-  static const bool on = [] {
-    const char* e = getenv("RFX_SELECT_FB");
-    return !(e && e[0] == '0');
-  }();
-  return on && D == 768 && (dtype == RFX_BF16 || dtype == RFX_F16);
-}
-
-int launch_screen_select_fb(const SelectFb& a, int D, int dtype, hipStream_t st) {
-  if (a.nq <= 0) return 0;
-  if (a.k < 1 || a.k > sel::kSelK || a.k > a.mp.k_lane || !a.diag || !a.ctl || !a.mp.ok) return -1;
-  if (D != 768 || a.nq > a.mp.nq_pad) return -1;
-  if (dtype == RFX_BF16) return selfb::launch_bf16_768(a, st);
-  if (dtype == RFX_F16) return selfb::launch_f16_768(a, st);
-  return -1;
 }
 
 }  // namespace rfx

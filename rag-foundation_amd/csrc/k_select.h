@@ -1,7 +1,6 @@
 // k_select.h — the two-pass scan's select: one 512-thread block takes one query's kept
 // candidates from kernel 10's lists, finds its survivors, re-scores them exactly from the stored rows and
-// writes the top-k.  A device function, so the select kernel (k_screen.hip) and the select with the exact
-// fallback inside its launch (k_select_fb.h) share one body; the LDS it uses is the caller's (SelLds).
+// writes the top-k.  A device function over the caller's LDS (SelLds); the select kernel is k_screen.hip's.
 #pragma once
 #include "k_mfma_common.h"
 
@@ -162,8 +161,8 @@ __device__ __forceinline__ bool select_body(const float* __restrict__ cs, const 
   if (sl.fail) {
     if (tid == 0) __hip_atomic_store(gate, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (diag && tid == 0) {
-      diag[q * 2] = nc;
-      diag[q * 2 + 1] = -1;
+      __hip_atomic_store(diag + q * 2, nc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(diag + q * 2 + 1, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return false;  // the exact fallback answers this query
   }
@@ -217,8 +216,8 @@ __device__ __forceinline__ bool select_body(const float* __restrict__ cs, const 
     }
   }
   if (diag && tid == 0) {
-    diag[q * 2] = nc;
-    diag[q * 2 + 1] = ns;
+    __hip_atomic_store(diag + q * 2, nc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(diag + q * 2 + 1, ns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   RFX_SEL_T(5)
   return true;

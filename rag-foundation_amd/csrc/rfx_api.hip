@@ -674,39 +674,6 @@ int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t
   }
   float* cs = (float*)(ws + L.cs_off);
   int32_t* cr = (int32_t*)(ws + L.cr_off);
-  if (L.fbk == 6 && rfx::select_fb_supported(ix.dim, ix.dtype)) {
-    // one launch: the select, and kernel 6 + the merge inside it when the select cannot prove a query
-    rfx::SelectFb a;
-    a.cs = scs;
-    a.cr = scr;
-    a.drops = drops;
-    a.n_lists = L.sp.n_lists;
-    a.list_len = L.sp.k_lane;
-    a.qe2 = qe2;
-    a.Qpad = qpad;
-    a.X = ix.data;
-    a.nq = nq;
-    a.k = k;
-    a.row_offset = row_offset;
-    a.out_s = out_s;
-    a.out_r = out_r;
-    a.out_rec = out_rec;
-    a.ctl = gate;
-    a.diag = diag;
-    a.force = ix.screen == 2;
-    a.mp = L.mp;
-    a.nrows = (int)ix.rows;
-    a.tau = tau;
-    a.fcs = cs;
-    a.fcr = cr;
-    a.n_cand = L.n_cand;
-    a.mask = mask;
-    a.rs = rfx::Rescore{ix.data, queries, ix.dim, ix.dtype, ix.rows};
-    if (rfx::launch_screen_select_fb(a, ix.dim, ix.dtype, st) != 0)
-      return fail(RFX_EUNSUPPORTED, "screen select k=%d unsupported", k);
-    RFX_HIP(hipGetLastError());
-    return RFX_OK;
-  }
   if (rfx::launch_screen_select(scs, scr, drops, L.sp.n_lists, L.sp.k_lane, qe2, qpad, ix.data, ix.dim, ix.dtype, nq,
                                 k, row_offset, out_s, out_r, out_rec, gate, diag, ix.screen == 2, st) != 0)
     return fail(RFX_EUNSUPPORTED, "screen select k=%d unsupported", k);

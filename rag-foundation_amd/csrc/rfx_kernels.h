@@ -167,41 +167,6 @@ int launch_screen_select(const float* cs, const int* cr, const uint32_t* drops, 
                          const float* qe2, const void* Q, const void* X, int D, int dtype, int64_t nq, int k,
                          int64_t row_offset, float* out_s, int64_t* out_r, void* out_rec, uint32_t* gate, int* diag,
                          int force, hipStream_t st);
-// The select with the exact fallback inside the same launch (k_select_fb.h; bf16 / f16 at d 768, fallback plan
-// kernel 6): replaces launch_screen_select + the gated kernel-6 scan + the gated merge of the same search.  ctl:
-// the search's 256-B gate area, zeroed by launch_screen_queries (word 0 the gate).  diag ([nq][2] ints) is
-// required: entry 2 q + 1 = -1 marks a query the fallback answers.
-struct SelectFb {
-  // the select (launch_screen_select's arguments)
-  const float* cs = nullptr;
-  const int* cr = nullptr;
-  const uint32_t* drops = nullptr;
-  int64_t n_lists = 0;
-  int list_len = 0;
-  const float* qe2 = nullptr;
-  const void* Qpad = nullptr;  // [kernel 6's nq_pad][D], 16-B aligned (the select and kernel 6 read it)
-  const void* X = nullptr;
-  int64_t nq = 0;
-  int k = 0;
-  int64_t row_offset = 0;
-  float* out_s = nullptr;
-  int64_t* out_r = nullptr;
-  void* out_rec = nullptr;
-  uint32_t* ctl = nullptr;
-  int* diag = nullptr;
-  int force = 0;
-  // the fallback: kernel 6's plan over the index rows, its threshold table, lists and merge
-  MfmaPlan mp{};
-  int nrows = 0;
-  uint32_t* tau = nullptr;
-  float* fcs = nullptr;
-  int* fcr = nullptr;
-  int64_t n_cand = 0;
-  const uint32_t* mask = nullptr;
-  Rescore rs{};
-};
-bool select_fb_supported(int D, int dtype);
-int launch_screen_select_fb(const SelectFb& a, int D, int dtype, hipStream_t st);
 
 // ---- embedding ---------------------------------------------------------------------------------
 void launch_embed_weights(int V, int dim, uint64_t seed, void* wt, hipStream_t st);
