@@ -176,8 +176,8 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   const int wave_g = blockIdx.x * 4 + w;
   const int wb = (int)min((int64_t)wave_g * rows_per_wave, (int64_t)nrows);
   const int we = (int)min((int64_t)wb + rows_per_wave, (int64_t)nrows);
-  // force bits 2/4/8/16/32 (RFX_K11_ABLATE, timing only, wrong results): no row stream / no query
-  // quantiser / no last-block work / no re-score and rank / no LB over the records
+  // force bits 2/4/8/16/32/64 (RFX_K11_ABLATE, timing only, wrong results): no row stream / no query
+  // quantiser / no last-block work / no re-score and rank / no LB over the records / no list offers
   const int T = (force & 2) ? 0 : we > wb ? (we - wb + 15) / 16 * 4 : 0;
   auto load_row = [&](int t, Codes<D>& v) {
     const int row = wb + 64 * (t >> 4) + 4 * (t & 15) + g;
@@ -335,6 +335,20 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       l.tr = readlane_i(l.lr, kK - 1);
     }
   };
+  // Round 6: a lone question's waves stream at most kKeepChunks 64-row chunks (config 2: 100 rows per wave);
+  // they keep every score in registers (one per lane per chunk) and pick their 16 best once, after the
+  // stream, instead of inserting into the sorted list chunk by chunk: the inserts' serial pop loop was ~12 of
+  // config 2's 39 us (RFX_K11_ABLATE=64, profiles/r06/k11_offer/).  The block record needs the wave's best
+  // 16 as a set (step 3 ranks all 64 entries) and the best score it did not keep.
+  constexpr int kKeepChunks = 2;
+  const bool keepall = NQT == 1 && rows_per_wave <= 64 * kKeepChunks;  // (block-uniform)
+  float ka[kKeepChunks];
+  int kr[kKeepChunks];
+#pragma unroll
+  for (int c = 0; c < kKeepChunks; ++c) {
+    ka[c] = __builtin_nanf("");
+    kr[c] = kEmptyRow;
+  }
   for (int t = 0; t < T; t += NB) {
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -344,13 +358,75 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
         // a 64-row chunk scored (or the last, partial one): every lane holds one row
         const int crow = wb + 64 * ((t + b) >> 4) + j * 4 + g;
         const bool ok = crow < we && (mask == nullptr || row_allowed(mask, crow));
+        if (keepall) {
+          // (the loop runs whole groups of NB iterations: a chunk end past T re-offers the last chunk's
+          // slot with nothing in it, which the list ignored; here it would overwrite the kept chunk)
+          const int ch = t + b < T ? (t + b) >> 4 : kKeepChunks;  // (< kKeepChunks within T)
 #pragma unroll
-        for (int qi = 0; qi < NQT; ++qi) {
-          offer(qi, ok ? cand[qi] : __builtin_nanf(""), crow);
-          cand[qi] = __builtin_nanf("");
+          for (int c = 0; c < kKeepChunks; ++c)
+            if (c == ch) {
+              ka[c] = ok ? cand[0] : __builtin_nanf("");
+              kr[c] = crow;
+            }
+          cand[0] = __builtin_nanf("");
+        } else {
+#pragma unroll
+          for (int qi = 0; qi < NQT; ++qi) {
+            if (!(force & 64)) offer(qi, ok ? cand[qi] : __builtin_nanf(""), crow);
+            cand[qi] = __builtin_nanf("");
+          }
         }
       }
     }
+  }
+  if (keepall) {
+    // the wave's 16 best as a set: v = the 16th largest orderable score (bitwise search on the counts of
+    // keys >= v; 0 = fewer than 16 rows), keep every key > v and ties at v in (chunk, lane) order up to 16;
+    // dm = the best score not kept (every row the wave drops is <= it, as the list's drop bound)
+    __shared__ float ksa[4][kK];
+    __shared__ int ksr[4][kK];
+    uint32_t key[kKeepChunks];
+    int nvalid = 0;
+#pragma unroll
+    for (int c = 0; c < kKeepChunks; ++c) {
+      key[c] = ka[c] == ka[c] ? ord_f32(ka[c]) : 0u;  // (a valid score's key is > 0)
+      nvalid += (int)__popcll(__ballot(key[c] != 0u));
+    }
+    uint32_t v = 0u;
+    if (nvalid > kK) {
+      for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t c1 = v | (1u << bit);
+        int cnt = 0;
+#pragma unroll
+        for (int c = 0; c < kKeepChunks; ++c) cnt += (int)__popcll(__ballot(key[c] >= c1));
+        v = cnt >= kK ? c1 : v;
+      }
+    }
+    int room = kK;
+#pragma unroll
+    for (int c = 0; c < kKeepChunks; ++c) room -= (int)__popcll(__ballot(key[c] > v));
+    bool keep[kKeepChunks];
+    int base = 0;
+    float d = -__builtin_inff();
+#pragma unroll
+    for (int c = 0; c < kKeepChunks; ++c) {
+      const uint64_t tie = __ballot(v != 0u && key[c] == v);
+      const int ti = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(tie >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tie, 0u));
+      keep[c] = key[c] > v || (v != 0u && key[c] == v && ti < room);
+      room -= min((int)__popcll(tie), max(room, 0));
+      if (key[c] != 0u && !keep[c]) d = fmaxf(d, ka[c]);
+      const uint64_t kb = __ballot(keep[c]);
+      const int p = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(kb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)kb, 0u));
+      if (keep[c]) {
+        ksa[w][p] = ka[c];
+        ksr[w][p] = kr[c];
+      }
+      base += (int)__popcll(kb);
+    }
+    dm[0] = d;
+    __syncthreads();
+    L[0].ls = lane < base ? ksa[w][lane] : -__builtin_inff();
+    L[0].lr = lane < base ? ksr[w][lane] : kEmptyRow;
   }
 
   RFX_K11_T(2);

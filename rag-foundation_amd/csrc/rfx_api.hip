@@ -695,11 +695,12 @@ int screen_search(Index& ix, const SearchLayout& L, const void* queries, int64_t
 }
 
 // RFX_K11_ABLATE (profiling only; wrong results): kernel 11 phase-skip bits 2 (row stream), 4 (query
-// quantiser), 8 (last block's select), 16 (its re-score and rank), 32 (its a_k over the records)
+// quantiser), 8 (last block's select), 16 (its re-score and rank), 32 (its a_k over the records), 64 (the
+// waves' list offers)
 int k11_ablate() {
   static const int v = [] {
     const char* e = getenv("RFX_K11_ABLATE");
-    return e ? (atoi(e) & 62) : 0;
+    return e ? (atoi(e) & 126) : 0;
   }();
   return v;
 }
