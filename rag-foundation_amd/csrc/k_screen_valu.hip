@@ -650,8 +650,8 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     }
     const bool every = n <= 1024;
     const int m = (force & 32) ? 0 : every ? n : n_lists;  // <= 1024
+    uint32_t a0, a1, a2, a3;  // this lane's keys, sorted
     {
-      uint32_t a0, a1, a2, a3;
       uint32_t ak[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -676,28 +676,44 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       cx(ak[1], ak[3]);
       cx(ak[1], ak[2]);
       a0 = ak[0], a1 = ak[1], a2 = ak[2], a3 = ak[3];
-      if (lane < kK) fin[w * kK + lane] = 0u;
-      for (int it = 0; it < k_out; ++it) {
-        const uint32_t mx = wave_max_u32(a0);
-        const bool win = lane == (int)__builtin_ctzll(__ballot(a0 == mx));
-        a0 = win ? a1 : a0;
-        a1 = win ? a2 : a1;
-        a2 = win ? a3 : a2;
-        a3 = win ? 0u : a3;
-        if (lane == 0) fin[w * kK + it] = mx;
+      if (m > 256) {  // (several waves hold keys: each extracts its k best, wave 0 ranks the 4 k)
+        if (lane < kK) fin[w * kK + lane] = 0u;
+        for (int it = 0; it < k_out; ++it) {
+          const uint32_t mx = wave_max_u32(a0);
+          const bool win = lane == (int)__builtin_ctzll(__ballot(a0 == mx));
+          a0 = win ? a1 : a0;
+          a1 = win ? a2 : a1;
+          a2 = win ? a3 : a2;
+          a3 = win ? 0u : a3;
+          if (lane == 0) fin[w * kK + it] = mx;
+        }
       }
     }
     __syncthreads();
     if (w == 0) {
-      const uint32_t x = fin[lane];  // 4 kK = 64 finalists, one per lane
-      int ge = 0, gt = 0;
+      uint32_t lb = 0u;
+      if (m <= 256) {
+        // every key is wave 0's (config 2: 250 record heads): the k-th largest with multiplicity by a
+        // bitwise search on ballot counts (round 6; 0 when fewer than k keys), no finalists, no barrier
+        uint32_t v = 0u;
+        for (int bit = 31; bit >= 0; --bit) {
+          const uint32_t c1 = v | (1u << bit);
+          const int cnt = (int)(__popcll(__ballot(a0 >= c1)) + __popcll(__ballot(a1 >= c1)) +
+                                __popcll(__ballot(a2 >= c1)) + __popcll(__ballot(a3 >= c1)));
+          v = cnt >= k_out ? c1 : v;
+        }
+        lb = v;
+      } else {
+        const uint32_t x = fin[lane];  // 4 kK = 64 finalists, one per lane
+        int ge = 0, gt = 0;
 #pragma unroll 16
-      for (int i = 0; i < 4 * kK; ++i) {
-        const uint32_t v = fin[i];
-        ge += v >= x ? 1 : 0;
-        gt += v > x ? 1 : 0;
+        for (int i = 0; i < 4 * kK; ++i) {
+          const uint32_t v = fin[i];
+          ge += v >= x ? 1 : 0;
+          gt += v > x ? 1 : 0;
+        }
+        lb = x && gt < k_out && ge >= k_out ? x : 0u;
       }
-      uint32_t lb = x && gt < k_out && ge >= k_out ? x : 0u;
       // LB* = the larger of the two lower bounds of a_k: >= every LB_b the blocks re-scored against
       lb = max(wave_max_u32(lb), max(max(redg[0], redg[1]), max(redg[2], redg[3])));
       if (lane == 0) {
