@@ -600,22 +600,24 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   __shared__ uint32_t fin[4 * kK];
   if (tid == 0) fail = force & 1;
   for (int qi = 0; qi < nq; ++qi) {
-    // bulk copy into LDS with 8 loads per thread in flight (agent-scope loads are not batched by the
+    // bulk copy into LDS with all loads of a thread in flight (agent-scope loads are not batched by the
     // compiler: one at a time they cost a memory round trip each — measured 55 us for this select)
-    for (int base = 0; base < n; base += 256 * 8) {
-      uint32_t sv8[8];
-      int rv8[8];
+    // (16 per thread: config 2's 250 records of 16 in one round trip; the loads are unconditional, on a
+    // clamped index, so no branch and no drain sits between them)
+    constexpr int UL = 16;
+    for (int base = 0; base < n; base += 256 * UL) {
+      uint32_t sv8[UL];
+      int rv8[UL];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < UL; ++u) {
         const int i = base + u * 256 + tid;
-        if (i < n) {
-          sv8[u] = __hip_atomic_load((const uint32_t*)cand_s + (int64_t)qi * n + i, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-          rv8[u] = __hip_atomic_load(cand_r + (int64_t)qi * n + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        const int ic = i < n ? i : n - 1;
+        sv8[u] = __hip_atomic_load((const uint32_t*)cand_s + (int64_t)qi * n + ic, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        rv8[u] = __hip_atomic_load(cand_r + (int64_t)qi * n + ic, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < UL; ++u) {
         const int i = base + u * 256 + tid;
         if (i < n) {
           bs[i] = __uint_as_float(sv8[u]);
