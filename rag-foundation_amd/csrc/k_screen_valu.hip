@@ -129,7 +129,9 @@ __device__ __attribute__((noinline)) void k11_fallback(const void* X, int nrows,
   }
 }
 
-template <int DT, int D, int NQT>
+constexpr int kKeepChunks = 2;  // the kept-score waves' chunks of 64 rows (KEEP below)
+
+template <int DT, int D, int NQT, bool KEEP>
 __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restrict__ X8, const uint4* __restrict__ tmeta,
                                                           const uint32_t* __restrict__ stats, int nrows,
                                                           const void* __restrict__ X, const void* __restrict__ Q, int nq,
@@ -335,18 +337,20 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       l.tr = readlane_i(l.lr, kK - 1);
     }
   };
-  // Round 6: a lone question's waves stream at most kKeepChunks 64-row chunks (config 2: 100 rows per wave);
-  // they keep every score in registers (one per lane per chunk) and pick their 16 best once, after the
-  // stream, instead of inserting into the sorted list chunk by chunk: the inserts' serial pop loop was ~12 of
-  // config 2's 39 us (RFX_K11_ABLATE=64, profiles/r06/k11_offer/).  The block record needs the wave's best
-  // 16 as a set (step 3 ranks all 64 entries) and the best score it did not keep.
-  constexpr int kKeepChunks = 2;
-  const bool keepall = NQT == 1 && rows_per_wave <= 64 * kKeepChunks;  // (block-uniform)
-  float ka[kKeepChunks];
+  // Round 6 (KEEP: at most kKeepChunks 64-row chunks per wave, config 2: 100 rows): the waves keep every
+  // score in registers (one per lane, chunk and question) and pick their 16 best per question once, after
+  // the stream, instead of inserting into the sorted lists chunk by chunk: the inserts' serial pop loop was
+  // ~12 of config 2's 39 us and ~85-115 of 124-179 us at 2-8 questions (RFX_K11_ABLATE=64,
+  // profiles/r06/k11_offer/, k11_nq8/).  The block record needs a wave's best 16 as a set (step 3 ranks all
+  // 64 entries) and the best score it did not keep.
+  constexpr bool keepall = KEEP;
+  static_assert(!KEEP || kKeepChunks >= 1, "");
+  float ka[NQT][kKeepChunks];
   int kr[kKeepChunks];
 #pragma unroll
   for (int c = 0; c < kKeepChunks; ++c) {
-    ka[c] = __builtin_nanf("");
+#pragma unroll
+    for (int qi = 0; qi < NQT; ++qi) ka[qi][c] = __builtin_nanf("");
     kr[c] = kEmptyRow;
   }
   for (int t = 0; t < T; t += NB) {
@@ -358,17 +362,19 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
         // a 64-row chunk scored (or the last, partial one): every lane holds one row
         const int crow = wb + 64 * ((t + b) >> 4) + j * 4 + g;
         const bool ok = crow < we && (mask == nullptr || row_allowed(mask, crow));
-        if (keepall) {
+        if constexpr (keepall) {
           // (the loop runs whole groups of NB iterations: a chunk end past T re-offers the last chunk's
           // slot with nothing in it, which the list ignored; here it would overwrite the kept chunk)
           const int ch = t + b < T ? (t + b) >> 4 : kKeepChunks;  // (< kKeepChunks within T)
 #pragma unroll
           for (int c = 0; c < kKeepChunks; ++c)
             if (c == ch) {
-              ka[c] = ok ? cand[0] : __builtin_nanf("");
+#pragma unroll
+              for (int qi = 0; qi < NQT; ++qi) ka[qi][c] = ok ? cand[qi] : __builtin_nanf("");
               kr[c] = crow;
             }
-          cand[0] = __builtin_nanf("");
+#pragma unroll
+          for (int qi = 0; qi < NQT; ++qi) cand[qi] = __builtin_nanf("");
         } else {
 #pragma unroll
           for (int qi = 0; qi < NQT; ++qi) {
@@ -379,54 +385,63 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
       }
     }
   }
-  if (keepall) {
-    // the wave's 16 best as a set: v = the 16th largest orderable score (bitwise search on the counts of
-    // keys >= v; 0 = fewer than 16 rows), keep every key > v and ties at v in (chunk, lane) order up to 16;
-    // dm = the best score not kept (every row the wave drops is <= it, as the list's drop bound)
-    __shared__ float ksa[4][kK];
-    __shared__ int ksr[4][kK];
-    uint32_t key[kKeepChunks];
-    int nvalid = 0;
+  if constexpr (keepall) {
+    // per question, the wave's 16 best as a set: v = the 16th largest orderable score (bitwise search on the
+    // counts of keys >= v; 0 = fewer than 16 rows), keep every key > v and ties at v in (chunk, lane) order
+    // up to 16; dm = the best score not kept (every row the wave drops is <= it, as the list's drop bound)
+    __shared__ float ksa[4][NQT][kK];
+    __shared__ int ksr[4][NQT][kK];
+    int nk[NQT];
 #pragma unroll
-    for (int c = 0; c < kKeepChunks; ++c) {
-      key[c] = ka[c] == ka[c] ? ord_f32(ka[c]) : 0u;  // (a valid score's key is > 0)
-      nvalid += (int)__popcll(__ballot(key[c] != 0u));
-    }
-    uint32_t v = 0u;
-    if (nvalid > kK) {
-      for (int bit = 31; bit >= 0; --bit) {
-        const uint32_t c1 = v | (1u << bit);
-        int cnt = 0;
+    for (int qi = 0; qi < NQT; ++qi) {
+      uint32_t key[kKeepChunks];
+      int nvalid = 0;
 #pragma unroll
-        for (int c = 0; c < kKeepChunks; ++c) cnt += (int)__popcll(__ballot(key[c] >= c1));
-        v = cnt >= kK ? c1 : v;
+      for (int c = 0; c < kKeepChunks; ++c) {
+        key[c] = ka[qi][c] == ka[qi][c] ? ord_f32(ka[qi][c]) : 0u;  // (a valid score's key is > 0)
+        nvalid += (int)__popcll(__ballot(key[c] != 0u));
       }
-    }
-    int room = kK;
+      uint32_t v = 0u;
+      if (nvalid > kK) {
+        for (int bit = 31; bit >= 0; --bit) {
+          const uint32_t c1 = v | (1u << bit);
+          int cnt = 0;
 #pragma unroll
-    for (int c = 0; c < kKeepChunks; ++c) room -= (int)__popcll(__ballot(key[c] > v));
-    bool keep[kKeepChunks];
-    int base = 0;
-    float d = -__builtin_inff();
-#pragma unroll
-    for (int c = 0; c < kKeepChunks; ++c) {
-      const uint64_t tie = __ballot(v != 0u && key[c] == v);
-      const int ti = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(tie >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tie, 0u));
-      keep[c] = key[c] > v || (v != 0u && key[c] == v && ti < room);
-      room -= min((int)__popcll(tie), max(room, 0));
-      if (key[c] != 0u && !keep[c]) d = fmaxf(d, ka[c]);
-      const uint64_t kb = __ballot(keep[c]);
-      const int p = base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(kb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)kb, 0u));
-      if (keep[c]) {
-        ksa[w][p] = ka[c];
-        ksr[w][p] = kr[c];
+          for (int c = 0; c < kKeepChunks; ++c) cnt += (int)__popcll(__ballot(key[c] >= c1));
+          v = cnt >= kK ? c1 : v;
+        }
       }
-      base += (int)__popcll(kb);
+      int room = kK;
+#pragma unroll
+      for (int c = 0; c < kKeepChunks; ++c) room -= (int)__popcll(__ballot(key[c] > v));
+      int base = 0;
+      float d = -__builtin_inff();
+#pragma unroll
+      for (int c = 0; c < kKeepChunks; ++c) {
+        const uint64_t tie = __ballot(v != 0u && key[c] == v);
+        const int ti =
+            (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(tie >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tie, 0u));
+        const bool keep = key[c] > v || (v != 0u && key[c] == v && ti < room);
+        room -= min((int)__popcll(tie), max(room, 0));
+        if (key[c] != 0u && !keep) d = fmaxf(d, ka[qi][c]);
+        const uint64_t kb = __ballot(keep);
+        const int p =
+            base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(kb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)kb, 0u));
+        if (keep) {
+          ksa[w][qi][p] = ka[qi][c];
+          ksr[w][qi][p] = kr[c];
+        }
+        base += (int)__popcll(kb);
+      }
+      dm[qi] = d;
+      nk[qi] = base;
     }
-    dm[0] = d;
     __syncthreads();
-    L[0].ls = lane < base ? ksa[w][lane] : -__builtin_inff();
-    L[0].lr = lane < base ? ksr[w][lane] : kEmptyRow;
+#pragma unroll
+    for (int qi = 0; qi < NQT; ++qi) {
+      L[qi].ls = lane < nk[qi] ? ksa[w][qi][lane] : -__builtin_inff();
+      L[qi].lr = lane < nk[qi] ? ksr[w][qi][lane] : kEmptyRow;
+    }
   }
 
   RFX_K11_T(2);
@@ -860,9 +875,19 @@ int launch_screen_valu(const ValuPlan& p, const int8_t* X8, const void* tmeta, c
   const dim3 grid((unsigned)p.blocks);
   uint32_t* const vtau = vstate;
   uint32_t* const vctr = vstate ? vstate + kValuFusedMaxNq : nullptr;
-#define RFX_SV(DTV, DV, NQ)                                                                                      \
-  hipLaunchKernelGGL((screen_valu_kernel<DTV, DV, NQ>), grid, dim3(256), 0, st, X8, (const uint4*)tmeta, stats, nrows, \
-                     X, Q, nq, p.rows_per_wave, mask, state, cs, cr, cx, k, out_s, out_r, force, vtau, vctr)
+  // the kept-score waves (KEEP) when every wave streams at most kKeepChunks 64-row chunks
+  const bool keep = p.rows_per_wave <= 64 * kKeepChunks;
+#define RFX_SV(DTV, DV, NQ)                                                                                         \
+  do {                                                                                                              \
+    if (keep)                                                                                                       \
+      hipLaunchKernelGGL((screen_valu_kernel<DTV, DV, NQ, true>), grid, dim3(256), 0, st, X8, (const uint4*)tmeta,    \
+                         stats, nrows, X, Q, nq, p.rows_per_wave, mask, state, cs, cr, cx, k, out_s, out_r, force,    \
+                         vtau, vctr);                                                                               \
+    else                                                                                                            \
+      hipLaunchKernelGGL((screen_valu_kernel<DTV, DV, NQ, false>), grid, dim3(256), 0, st, X8, (const uint4*)tmeta,   \
+                         stats, nrows, X, Q, nq, p.rows_per_wave, mask, state, cs, cr, cx, k, out_s, out_r, force,    \
+                         vtau, vctr);                                                                               \
+  } while (0)
 #define RFX_SV_D(DTV)                  \
   if (D == 768) {                      \
     if (nq == 1)                       \
