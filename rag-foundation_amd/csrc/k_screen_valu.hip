@@ -344,7 +344,10 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
   // profiles/r06/k11_offer/, k11_nq8/).  The block record needs a wave's best 16 as a set (step 3 ranks all
   // 64 entries) and the best score it did not keep.
   constexpr bool keepall = KEEP;
-  static_assert(!KEEP || kKeepChunks >= 1, "");
+  // a lone question's list path (> kKeepChunks chunks per wave) seeds its sorted list by one selection over
+  // its first kKeepChunks kept chunks (300k rows: 60.8 -> 53.4 us, 1M: 147.5 -> 140.0 us); with 8 query
+  // slots the seeded lists measured slower at 1M rows (0.59 against 0.39 ms) and are not used
+  constexpr bool seeded = !KEEP && NQT == 1;
   float ka[NQT][kKeepChunks];
   int kr[kKeepChunks];
 #pragma unroll
@@ -353,42 +356,13 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
     for (int qi = 0; qi < NQT; ++qi) ka[qi][c] = __builtin_nanf("");
     kr[c] = kEmptyRow;
   }
-  for (int t = 0; t < T; t += NB) {
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      load_row(t + b + NB - 1, buf[(b + NB - 1) % NB]);  // past T: re-reads of row wb, never offered
-      score_row(t + b, buf[b]);
-      if ((b & 3) == 3 && (((t + b + 1) & 15) == 0 || t + b + 1 >= T)) {
-        // a 64-row chunk scored (or the last, partial one): every lane holds one row
-        const int crow = wb + 64 * ((t + b) >> 4) + j * 4 + g;
-        const bool ok = crow < we && (mask == nullptr || row_allowed(mask, crow));
-        if constexpr (keepall) {
-          // (the loop runs whole groups of NB iterations: a chunk end past T re-offers the last chunk's
-          // slot with nothing in it, which the list ignored; here it would overwrite the kept chunk)
-          const int ch = t + b < T ? (t + b) >> 4 : kKeepChunks;  // (< kKeepChunks within T)
-#pragma unroll
-          for (int c = 0; c < kKeepChunks; ++c)
-            if (c == ch) {
-#pragma unroll
-              for (int qi = 0; qi < NQT; ++qi) ka[qi][c] = ok ? cand[qi] : __builtin_nanf("");
-              kr[c] = crow;
-            }
-#pragma unroll
-          for (int qi = 0; qi < NQT; ++qi) cand[qi] = __builtin_nanf("");
-        } else {
-#pragma unroll
-          for (int qi = 0; qi < NQT; ++qi) {
-            if (!(force & 64)) offer(qi, ok ? cand[qi] : __builtin_nanf(""), crow);
-            cand[qi] = __builtin_nanf("");
-          }
-        }
-      }
-    }
-  }
-  if constexpr (keepall) {
-    // per question, the wave's 16 best as a set: v = the 16th largest orderable score (bitwise search on the
-    // counts of keys >= v; 0 = fewer than 16 rows), keep every key > v and ties at v in (chunk, lane) order
-    // up to 16; dm = the best score not kept (every row the wave drops is <= it, as the list's drop bound)
+  // Per question, the wave's 16 best kept scores as a set: v = the 16th largest orderable score (bitwise
+  // search on the counts of keys >= v; 0 = fewer than 16 rows), keep every key > v and ties at v in (chunk,
+  // lane) order up to 16, into lanes 0..15 of the list; dm = the best score not kept (every row the wave
+  // drops is <= it, as the list's drop bound).  sort: also order the 16 (score desc, row asc; a bitonic
+  // network over lanes) and set the list's threshold, for the list inserts of later chunks.  Wave-local:
+  // the compaction goes through this wave's LDS rows only (no block barrier: waves stream different counts).
+  auto select_kept = [&](bool sort) {
     __shared__ float ksa[4][NQT][kK];
     __shared__ int ksr[4][NQT][kK];
     int nk[NQT];
@@ -432,17 +406,76 @@ __global__ __launch_bounds__(256) void screen_valu_kernel(const int8_t* __restri
           ksr[w][qi][p] = kr[c];
         }
         base += (int)__popcll(kb);
+        ka[qi][c] = __builtin_nanf("");
       }
-      dm[qi] = d;
+      dm[qi] = fmaxf(dm[qi], d);
       nk[qi] = base;
     }
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int qi = 0; qi < NQT; ++qi) {
-      L[qi].ls = lane < nk[qi] ? ksa[w][qi][lane] : -__builtin_inff();
-      L[qi].lr = lane < nk[qi] ? ksr[w][qi][lane] : kEmptyRow;
+      float ls = lane < nk[qi] ? ksa[w][qi][lane] : -__builtin_inff();
+      int lr = lane < nk[qi] ? ksr[w][qi][lane] : kEmptyRow;
+      if (sort) {
+#pragma unroll
+        for (int kk = 2; kk <= kK; kk <<= 1)
+#pragma unroll
+          for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+            const float ps = __shfl_xor(ls, jj);
+            const int pr = __shfl_xor(lr, jj);
+            const bool lower = (lane & jj) == 0, desc = (lane & kk) == 0;
+            const bool mine = better(ls, lr, ps, pr);
+            if (lower == desc ? !mine : mine) {
+              ls = ps;
+              lr = pr;
+            }
+          }
+        L[qi].ts = readlane_f(ls, kK - 1);
+        L[qi].tr = readlane_i(lr, kK - 1);
+      }
+      L[qi].ls = ls;
+      L[qi].lr = lr;
+    }
+    __builtin_amdgcn_wave_barrier();  // (this wave's LDS rows are read before any later rewrite)
+  };
+  for (int t = 0; t < T; t += NB) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      load_row(t + b + NB - 1, buf[(b + NB - 1) % NB]);  // past T: re-reads of row wb, never offered
+      score_row(t + b, buf[b]);
+      if ((b & 3) == 3 && (((t + b + 1) & 15) == 0 || t + b + 1 >= T)) {
+        // a 64-row chunk scored (or the last, partial one): every lane holds one row
+        const int crow = wb + 64 * ((t + b) >> 4) + j * 4 + g;
+        const bool ok = crow < we && (mask == nullptr || row_allowed(mask, crow));
+        // (the loop runs whole groups of NB iterations: a chunk end past T re-offers the last chunk's slot
+        // with nothing in it, which the list ignores; kept, it would overwrite the kept chunk)
+        const int ch = t + b < T ? (t + b) >> 4 : 1 << 20;
+        if (keepall || (seeded && ch < kKeepChunks)) {
+          // KEEP: every chunk; a seeded list: the first kKeepChunks, then one selection seeds the sorted
+          // list (most inserts happen in the first chunks, before a list's threshold has risen)
+#pragma unroll
+          for (int c = 0; c < kKeepChunks; ++c)
+            if (c == ch) {
+#pragma unroll
+              for (int qi = 0; qi < NQT; ++qi) ka[qi][c] = ok ? cand[qi] : __builtin_nanf("");
+              kr[c] = crow;
+            }
+#pragma unroll
+          for (int qi = 0; qi < NQT; ++qi) cand[qi] = __builtin_nanf("");
+          if (seeded && ch == kKeepChunks - 1) select_kept(true);
+        } else {
+#pragma unroll
+          for (int qi = 0; qi < NQT; ++qi) {
+            if (!(force & 64)) offer(qi, ok ? cand[qi] : __builtin_nanf(""), crow);
+            cand[qi] = __builtin_nanf("");
+          }
+        }
+      }
     }
   }
+  // KEEP: every chunk was kept; a seeded list of at most one chunk has not selected yet
+  if (keepall || (seeded && T <= 16)) select_kept(false);
 
   RFX_K11_T(2);
   // ---- 3. block record per query: the 15 best A of the block (rows), and its drop bound ----------

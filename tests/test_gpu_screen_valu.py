@@ -85,6 +85,22 @@ def test_config2_shape(rindex):
         _check(ix, rows32, q[i:i + 1].contiguous(), q32[i:i + 1], 10)
 
 
+@pytest.mark.parametrize("dtype,nq,k", [("f32", 1, 10), ("f32", 8, 10), ("bf16", 3, 16)])
+def test_kernel11_list_path_larger_store(rindex, dtype, nq, k):
+    """More than 128 rows per wave (200k rows, ~200 per wave): the waves keep their first two 64-row chunks'
+    scores, select and sort their 16 best, and insert the later chunks into those sorted lists (round 6);
+    ties at the kept set's edge included (duplicated rows)."""
+    ix, rows32 = _make(rindex, 200_000, 768, dtype)
+    assert ix.search_plan(nq, k) == 11
+    q, q32 = _queries(rindex, nq, 768, dtype, seed=7)
+    _check(ix, rows32, q, q32, k)
+    top = int(osearch.topk(q32[:1].astype(np.float64), rows32.astype(np.float64), 1)[1][0, 0])
+    ix.add(ix.read(top, 1).repeat(30, 1))  # 30 copies of query 0's winner: ties at every wave's 16th
+    rows32 = np.concatenate([rows32, np.repeat(rows32[top:top + 1], 30, axis=0)])
+    _check(ix, rows32, q, q32, k)
+    ix.close()
+
+
 def test_kernel11_fallback_and_exact_agree(rindex):
     ix, rows32 = _make(rindex, 40000, 768, "f32")
     q, q32 = _queries(rindex, 4, 768, "f32")
