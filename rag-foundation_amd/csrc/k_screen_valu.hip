@@ -921,17 +921,30 @@ int launch_screen_valu(const ValuPlan& p, const int8_t* X8, const void* tmeta, c
                          stats, nrows, X, Q, nq, p.rows_per_wave, mask, state, cs, cr, cx, k, out_s, out_r, force,    \
                          vtau, vctr);                                                                               \
   } while (0)
-#define RFX_SV_D(DTV)                  \
-  if (D == 768) {                      \
-    if (nq == 1)                       \
-      RFX_SV(DTV, 768, 1);             \
-    else                               \
-      RFX_SV(DTV, 768, 8);             \
-  } else {                             \
-    if (nq == 1)                       \
-      RFX_SV(DTV, 1024, 1);            \
-    else                               \
-      RFX_SV(DTV, 1024, 8);            \
+  // (2 and 4 query slots for the kept-score waves: a batch of 2 paid the stream work of 8 slots — 32 of its
+  // 54 us, profiles/r06/k11_nq8_ablate/; the list path keeps 1 or 8)
+#define RFX_SV_KEEP(DTV, DV, NQ)                                                                                  \
+  hipLaunchKernelGGL((screen_valu_kernel<DTV, DV, NQ, true>), grid, dim3(256), 0, st, X8, (const uint4*)tmeta, stats, \
+                     nrows, X, Q, nq, p.rows_per_wave, mask, state, cs, cr, cx, k, out_s, out_r, force, vtau, vctr)
+#define RFX_SV_D(DTV)                            \
+  if (D == 768) {                                \
+    if (nq == 1)                                 \
+      RFX_SV(DTV, 768, 1);                       \
+    else if (keep && nq <= 2)                    \
+      RFX_SV_KEEP(DTV, 768, 2);                  \
+    else if (keep && nq <= 4)                    \
+      RFX_SV_KEEP(DTV, 768, 4);                  \
+    else                                         \
+      RFX_SV(DTV, 768, 8);                       \
+  } else {                                       \
+    if (nq == 1)                                 \
+      RFX_SV(DTV, 1024, 1);                      \
+    else if (keep && nq <= 2)                    \
+      RFX_SV_KEEP(DTV, 1024, 2);                 \
+    else if (keep && nq <= 4)                    \
+      RFX_SV_KEEP(DTV, 1024, 4);                 \
+    else                                         \
+      RFX_SV(DTV, 1024, 8);                      \
   }
   if (dtype == RFX_F32) {
     RFX_SV_D(RFX_F32)
@@ -941,6 +954,7 @@ int launch_screen_valu(const ValuPlan& p, const int8_t* X8, const void* tmeta, c
     RFX_SV_D(RFX_F16)
   }
 #undef RFX_SV_D
+#undef RFX_SV_KEEP
 #undef RFX_SV
   return 0;
 }

@@ -69,7 +69,7 @@ def test_f32_int8_copy_bit_exact(rindex):
 
 
 @pytest.mark.parametrize("dtype,d", [("f32", 768), ("bf16", 768), ("f16", 768), ("f32", 1024), ("bf16", 1024)])
-@pytest.mark.parametrize("nq,k", [(1, 10), (3, 5), (8, 16)])
+@pytest.mark.parametrize("nq,k", [(1, 10), (2, 10), (3, 5), (4, 12), (8, 16)])
 def test_kernel11_matches_oracle(rindex, dtype, d, nq, k):
     ix, rows32 = _make(rindex, 30000, d, dtype)
     assert ix.search_plan(nq, k) == 11
