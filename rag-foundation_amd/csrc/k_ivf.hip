@@ -523,6 +523,96 @@ __global__ __launch_bounds__(1024) void group_pairs_kernel(const int64_t* __rest
 // top-K list per query.  Candidates: cand[((q * nprobe + j) * S + s) * 4 + wave][K] (every pair
 // of every list is written, empty lists too).
 constexpr int kQB = 8;
+constexpr int kSeedChunks = 2;
+
+// The K best of a wave's kept candidates per query, exactly as the sorted list would hold them: (score desc,
+// id asc), each query's K in lanes 0..K-1, sorted, and the list's threshold set (WaveList).  v = the K-th
+// largest orderable score (bitwise search on ballot counts); ties at v are taken by the smallest ids (a second
+// bitwise search over the tied ids), so the set is the list's set whatever the order the rows came in.
+// Wave-local (LDS rows of this wave only).
+template <int K, int QB, int NCH>
+__device__ __forceinline__ void seed_lists(float (&ka)[QB][NCH], int (&kg)[NCH], WaveList<K> (&lst)[QB], int w) {
+  __shared__ float ssa[4][K];
+  __shared__ int ssr[4][K];
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int qi = 0; qi < QB; ++qi) {
+    uint32_t key[NCH];
+    int nvalid = 0;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      key[c] = ka[qi][c] == ka[qi][c] ? ord_f32(ka[qi][c]) : 0u;
+      nvalid += (int)__popcll(__ballot(key[c] != 0u));
+    }
+    uint32_t v = 0u;
+    if (nvalid > K)
+      for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t c1 = v | (1u << bit);
+        int cnt = 0;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) cnt += (int)__popcll(__ballot(key[c] >= c1));
+        v = cnt >= K ? c1 : v;
+      }
+    int room = K;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) room -= (int)__popcll(__ballot(key[c] > v));
+    // ties at v (v > 0 only): the room smallest ids, gid <= g2
+    uint32_t g2 = 0u;
+    if (v != 0u) {
+      int ntie = 0;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) ntie += (int)__popcll(__ballot(key[c] == v));
+      if (ntie > room) {
+        // g2 = the room-th smallest tied id: the largest value with fewer than room tied ids below it
+        for (int bit = 31; bit >= 0; --bit) {
+          const uint32_t c1 = g2 | (1u << bit);
+          int cnt = 0;
+#pragma unroll
+          for (int c = 0; c < NCH; ++c) cnt += (int)__popcll(__ballot(key[c] == v && (uint32_t)kg[c] < c1));
+          g2 = cnt < room ? c1 : g2;
+        }
+      } else {
+        g2 = 0xffffffffu;
+      }
+    }
+    int base = 0;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const bool keep = key[c] > v || (v != 0u && key[c] == v && (uint32_t)kg[c] <= g2);
+      const uint64_t kb = __ballot(keep);
+      const int p =
+          base + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(kb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)kb, 0u));
+      if (keep) {
+        ssa[w][p] = ka[qi][c];
+        ssr[w][p] = kg[c];
+      }
+      base += (int)__popcll(kb);
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    float ls = lane < base ? ssa[w][lane] : -__builtin_inff();
+    int lr = lane < base ? ssr[w][lane] : kEmptyRow;
+    __builtin_amdgcn_wave_barrier();  // (read before the next query's compaction rewrites the rows)
+#pragma unroll
+    for (int kk = 2; kk <= K; kk <<= 1)
+#pragma unroll
+      for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+        const float ps = __shfl_xor(ls, jj);
+        const int pr = __shfl_xor(lr, jj);
+        const bool lower = (lane & jj) == 0, desc = (lane & kk) == 0;
+        const bool mine = better(ls, lr, ps, pr);
+        if (lower == desc ? !mine : mine) {
+          ls = ps;
+          lr = pr;
+        }
+      }
+    lst[qi].ls = lane < K ? ls : -__builtin_inff();
+    lst[qi].lr = lane < K ? lr : kEmptyRow;
+    lst[qi].ts = readlane_f(ls, K - 1);
+    lst[qi].tr = readlane_i(lr, K - 1);
+  }
+}
+
 template <int K, int NC>
 __global__ __launch_bounds__(256) void list_scan_kernel(const int8_t* __restrict__ codes, const float* __restrict__ inv,
                                                         const int* __restrict__ ids, const int64_t* __restrict__ off,
@@ -551,6 +641,19 @@ __global__ __launch_bounds__(256) void list_scan_kernel(const int8_t* __restrict
     WaveList<K> lst[kQB];
 #pragma unroll
     for (int qi = 0; qi < kQB; ++qi) lst[qi].init();
+    // Round 6: a wave's first kSeedChunks 64-row chunks are kept in registers (score per lane, chunk and
+    // query; the id per lane and chunk) and seed each query's sorted list by one selection (seed_lists), the
+    // later chunks go through the list inserts.  A config-5 wave streams ~3 chunks of a list per batch, so the
+    // inserts of its first chunks — nearly every candidate, the list still empty — were most of them.
+    float ka[kQB][kSeedChunks];
+    int kg[kSeedChunks];
+    int nch = 0;  // chunks this wave has scored in this batch (wave-uniform)
+#pragma unroll
+    for (int c = 0; c < kSeedChunks; ++c) {
+#pragma unroll
+      for (int qi = 0; qi < kQB; ++qi) ka[qi][c] = __builtin_nanf("");
+      kg[c] = kEmptyRow;
+    }
     for (int64_t base = r0 + (int64_t)(sp * 4 + w) * 64; base < r1; base += 256 * S) {
       float cand[kQB];
 #pragma unroll
@@ -584,10 +687,23 @@ __global__ __launch_bounds__(256) void list_scan_kernel(const int8_t* __restrict
       const int64_t cr = valid ? crow : r0;
       const float ir = inv[cr];
       const int gid = ids[cr];
+      if (nch < kSeedChunks) {
 #pragma unroll
-      for (int qi = 0; qi < kQB; ++qi)
-        if (qi < nb) lst[qi].offer(__fmul_rn(cand[qi], __fmul_rn(ir, qf[qi])), gid, valid);
+        for (int c = 0; c < kSeedChunks; ++c)
+          if (c == nch) {
+#pragma unroll
+            for (int qi = 0; qi < kQB; ++qi)
+              ka[qi][c] = valid && qi < nb ? __fmul_rn(cand[qi], __fmul_rn(ir, qf[qi])) : __builtin_nanf("");
+            kg[c] = gid;
+          }
+        if (++nch == kSeedChunks) seed_lists<K, kQB, kSeedChunks>(ka, kg, lst, w);
+      } else {
+#pragma unroll
+        for (int qi = 0; qi < kQB; ++qi)
+          if (qi < nb) lst[qi].offer(__fmul_rn(cand[qi], __fmul_rn(ir, qf[qi])), gid, valid);
+      }
     }
+    if (nch < kSeedChunks) seed_lists<K, kQB, kSeedChunks>(ka, kg, lst, w);  // (fewer chunks than kept)
     if (lane < K) {
 #pragma unroll
       for (int qi = 0; qi < kQB; ++qi) {
