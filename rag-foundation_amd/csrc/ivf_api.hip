@@ -41,7 +41,7 @@ struct Ivf {
   int* labels = nullptr;    // [cap]
   bool dirty = true;        // posting lists stale
   int64_t lcap = 0;
-  int8_t* lcodes = nullptr;  // [lcap][dim], list order
+  int8_t* lcodes = nullptr;  // [lcap rounded up to 64][dim], list order, 64-row blocks chunk-major
   float* linv = nullptr;
   int* lids = nullptr;
   int64_t* off = nullptr;  // [nlist + 1]
@@ -104,7 +104,9 @@ int build(Ivf& iv, hipStream_t st) {
       if (p) IVF_HIP(hipFree(p));
     iv.lcodes = nullptr, iv.linv = nullptr, iv.lids = nullptr;
     const int64_t c = std::max<int64_t>(iv.cap, 1);
-    if (hipMalloc(&iv.lcodes, (size_t)c * iv.dim) != hipSuccess || hipMalloc(&iv.linv, (size_t)c * 4) != hipSuccess ||
+    // (the list-order codes in whole 64-row blocks: k_ivf.hip gather_rows_kernel)
+    if (hipMalloc(&iv.lcodes, (size_t)((c + 63) / 64 * 64) * iv.dim) != hipSuccess ||
+        hipMalloc(&iv.linv, (size_t)c * 4) != hipSuccess ||
         hipMalloc(&iv.lids, (size_t)c * 4) != hipSuccess)
       return api_fail(RFX_ENOMEM, "hipMalloc failed for posting lists (%lld rows)", (long long)c);
     iv.lcap = c;

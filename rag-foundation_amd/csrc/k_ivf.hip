@@ -431,7 +431,10 @@ __global__ __launch_bounds__(1024) void offsets_kernel(const int* __restrict__ c
   if (t == 1023) off[m] = part[1023];
 }
 
-// list-order copy of codes and scales: dst row p = src row ids[p] (one wave per row)
+// list-order copy of codes and scales: dst row p = src row ids[p] (one wave per row).  Round 6: the
+// list-order codes are stored in 64-row blocks, chunk-major: 16-B chunk c of row p at
+// (p / 64) * 64 D + c * 1024 + (p % 64) * 16, so the list scan's lane-per-row loads are 1-KB runs
+// (kBlockRows rows of one chunk) and every lane holds a whole row's dot (list_scan_kernel).
 __global__ __launch_bounds__(256) void gather_rows_kernel(const int8_t* __restrict__ codes,
                                                           const float* __restrict__ inv,
                                                           const int* __restrict__ ids, int64_t n, int D,
@@ -442,7 +445,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(const int8_t* __restri
   for (int64_t p = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; p < n; p += nwaves) {
     const int64_t src = ids[p];
     for (int c = lane; c < nch; c += 64)
-      *(uint4*)(dcodes + p * D + c * 16) = *(const uint4*)(codes + src * D + c * 16);
+      *(uint4*)(dcodes + (p >> 6) * 64 * D + c * 1024 + (p & 63) * 16) = *(const uint4*)(codes + src * D + c * 16);
     if (lane == 0) dinv[p] = inv[src];
   }
 }
@@ -620,22 +623,27 @@ __global__ __launch_bounds__(256) void list_scan_kernel(const int8_t* __restrict
                                                         int nprobe, const int8_t* __restrict__ qq,
                                                         const float* __restrict__ qinv, float* __restrict__ cand_s,
                                                         int* __restrict__ cand_r) {
-  constexpr int D = NC * 256;
-  __shared__ __attribute__((aligned(16))) int8_t qs[kQB][D];
+  constexpr int D = NC * 256, NCH = D / 16;  // 16-B chunks per row
+  // Round 6: one lane per row.  The codes are in 64-row blocks, chunk-major (gather_rows_kernel), so a wave's
+  // load of chunk c of its 64 rows is one 1-KB run; the batch's queries are wave-uniform and come through
+  // scalar loads (SGPR operands of v_dot4), so no LDS reads, and every lane ends with its row's whole dot
+  // for each query (no cross-lane sums).  Before, 16 lanes shared a row: per 4 rows a wave read 8 KB of
+  // staged queries from LDS and summed 8 dots over 16 lanes (DPP), the list scan at 5.3 TB/s.
+  constexpr int G = 4;  // chunks per load group (double-buffered)
+  static_assert(NCH % G == 0, "chunk groups");
+  constexpr int NG = NCH / G;
   __shared__ float qf[kQB];
   const int L = blockIdx.x, S = gridDim.y, sp = blockIdx.y;
   const int p0 = pair_off[L], p1 = pair_off[L + 1];
   if (p0 == p1) return;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, j = lane & 15;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int64_t r0 = off[L], r1 = off[L + 1];
   for (int pb = p0; pb < p1; pb += kQB) {
     const int nb = min(kQB, p1 - pb);
-    for (int i = tid; i < kQB * (D / 16); i += 256) {
-      const int qi = i / (D / 16), c = i - qi * (D / 16);
-      uint4 v = uint4{0u, 0u, 0u, 0u};
-      if (qi < nb) v = *(const uint4*)(qq + (int64_t)(pairs[pb + qi] / nprobe) * D + c * 16);
-      *(uint4*)(&qs[qi][c * 16]) = v;
-    }
+    const uint4* qv[kQB];
+#pragma unroll
+    for (int qi = 0; qi < kQB; ++qi)
+      qv[qi] = (const uint4*)(qq + (int64_t)(pairs[pb + (qi < nb ? qi : 0)] / nprobe) * D);
     if (tid < kQB) qf[tid] = tid < nb ? qinv[pairs[pb + tid] / nprobe] : 0.f;
     __syncthreads();
     WaveList<K> lst[kQB];
@@ -655,36 +663,41 @@ __global__ __launch_bounds__(256) void list_scan_kernel(const int8_t* __restrict
       kg[c] = kEmptyRow;
     }
     for (int64_t base = r0 + (int64_t)(sp * 4 + w) * 64; base < r1; base += 256 * S) {
-      float cand[kQB];
+      const int64_t crow = base + lane;
+      const bool valid = crow < r1;
+      const int64_t cr = valid ? crow : r0;  // in-list row (never past the list)
+      const int8_t* rp = codes + (cr >> 6) * (64 * D) + (cr & 63) * 16;  // chunk c at rp + c * 1024
+      int acc[kQB];
 #pragma unroll
-      for (int qi = 0; qi < kQB; ++qi) cand[qi] = 0.f;
-#pragma unroll 2
-      for (int it = 0; it < 16; ++it) {
-        const int64_t row = base + it * 4 + g;
-        const int64_t rr = row < r1 ? row : r0;  // in-list row (never past the list)
-        uint4 v[NC];
+      for (int qi = 0; qi < kQB; ++qi) acc[qi] = 0;
+      uint4 va[G], vb[G];
 #pragma unroll
-        for (int i = 0; i < NC; ++i) v[i] = *(const uint4*)(codes + rr * D + (j + 16 * i) * 16);
+      for (int c = 0; c < G; ++c) va[c] = *(const uint4*)(rp + c * 1024);
+#pragma unroll
+      for (int cg = 0; cg < NG; ++cg) {
+        uint4(&cur)[G] = (cg & 1) ? vb : va;
+        uint4(&nxt)[G] = (cg & 1) ? va : vb;
+        if (cg + 1 < NG) {
+#pragma unroll
+          for (int c = 0; c < G; ++c) nxt[c] = *(const uint4*)(rp + ((cg + 1) * G + c) * 1024);
+        }
 #pragma unroll
         for (int qi = 0; qi < kQB; ++qi) {
           if (qi < nb) {
-            int acc = 0;
 #pragma unroll
-            for (int i = 0; i < NC; ++i) {
-              const uint4 q = *(const uint4*)(&qs[qi][(j + 16 * i) * 16]);
-              acc = __builtin_amdgcn_sdot4((int)v[i].x, (int)q.x, acc, false);
-              acc = __builtin_amdgcn_sdot4((int)v[i].y, (int)q.y, acc, false);
-              acc = __builtin_amdgcn_sdot4((int)v[i].z, (int)q.z, acc, false);
-              acc = __builtin_amdgcn_sdot4((int)v[i].w, (int)q.w, acc, false);
+            for (int c = 0; c < G; ++c) {
+              const uint4 q = qv[qi][cg * G + c];
+              acc[qi] = __builtin_amdgcn_sdot4((int)cur[c].x, (int)q.x, acc[qi], false);
+              acc[qi] = __builtin_amdgcn_sdot4((int)cur[c].y, (int)q.y, acc[qi], false);
+              acc[qi] = __builtin_amdgcn_sdot4((int)cur[c].z, (int)q.z, acc[qi], false);
+              acc[qi] = __builtin_amdgcn_sdot4((int)cur[c].w, (int)q.w, acc[qi], false);
             }
-            const float d = row16_sum((float)acc);  // integer partial sums < 2^24: exact
-            if (j == it) cand[qi] = d;
           }
         }
       }
-      const int64_t crow = base + j * 4 + g;
-      const bool valid = crow < r1;
-      const int64_t cr = valid ? crow : r0;
+      float cand[kQB];  // |dot| <= 768 * 127 * 127 < 2^24: exact in f32, the value the 16-lane sum had
+#pragma unroll
+      for (int qi = 0; qi < kQB; ++qi) cand[qi] = (float)acc[qi];
       const float ir = inv[cr];
       const int gid = ids[cr];
       if (nch < kSeedChunks) {
