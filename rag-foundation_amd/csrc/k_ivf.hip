@@ -205,10 +205,37 @@ __global__ __launch_bounds__(256, 1) void coarse_kernel(const int8_t* __restrict
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = mfma_i8(a[mi], b[ni], acc[mi][ni]);
+        for (int ni = 0; ni < 2; ++ni) {
+          // MODE 0: X rows as accumulator rows, centroids as lanes, so the score rows go out in 128-B runs
+          if constexpr (MODE == 0)
+            acc[mi][ni] = mfma_i8(b[ni], a[mi], acc[mi][ni]);
+          else
+            acc[mi][ni] = mfma_i8(a[mi], b[ni], acc[mi][ni]);
+        }
     }
     if (t + 1 < T) store_c((t + 1) & 1, nv);
-    if (kc == nk - 1) {
+    if (MODE == 0 && kc == nk - 1) {
+      // round 6: lane l32 holds centroid cbase + 32 mi + l32 for 16 X rows, so each store of a row's scores
+      // is 32 consecutive floats (before: a lane per X row, 16-KB strides between lanes; 43.7 us per batch)
+      const int cbase = (ct0 + t / nk) * kCT + wm * 64;
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        const int c = cbase + mi * 32 + l32;
+        const bool cok = c < m;
+        const float fcc = cok ? fc[c] : 0.f;
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int64_t x = x0 + wn * 64 + ni * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (cok && x < n) {
+              out_s[x * m + c] = __fmul_rn((float)acc[mi][ni][r], fcc);
+              out_i[x * m + c] = c;
+            }
+          }
+      }
+    }
+    if (MODE == 1 && kc == nk - 1) {
       const int cbase = (ct0 + t / nk) * kCT + wm * 64;
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
@@ -220,12 +247,7 @@ __global__ __launch_bounds__(256, 1) void coarse_kernel(const int8_t* __restrict
             const int c = cbase + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
             if (c < m) {
               const float f = __fmul_rn((float)acc[mi][ni][r], fc[c]);
-              if constexpr (MODE == 0) {
-                if (x < n) {
-                  out_s[x * m + c] = f;
-                  out_i[x * m + c] = c;
-                }
-              } else if (f > bs[ni] || (f == bs[ni] && c < bc[ni])) {
+              if (f > bs[ni] || (f == bs[ni] && c < bc[ni])) {
                 bs[ni] = f;
                 bc[ni] = c;
               }
