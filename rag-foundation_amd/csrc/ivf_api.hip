@@ -439,7 +439,10 @@ int rfx_ivf_search(rfx_ivf_t h, const void* queries_d, int64_t nq, int dtype, in
   if (rfx::ivf::launch_list_scan(L.K, iv->dim, iv->nlist, L.splits, iv->lcodes, iv->linv, iv->lids, iv->off, poff, pairs, nprobe,
                                  qq, qinv, cs, cr, st))
     return api_fail(RFX_EUNSUPPORTED, "list scan launch rejected (k=%d dim=%d)", k, iv->dim);
-  if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.ncand, L.K, k, 0, out_scores_d, out_rows_d, nullptr, st))
+  // (the wave lists are sorted best first, empty slots last: the merge reads each only as far as it can
+  // still admit)
+  if (rfx::launch_topk_merge_lists(cs, cr, 0, nq, L.ncand, L.K, k, 0, out_scores_d, out_rows_d, nullptr, st,
+                                   /*sorted=*/true))
     return api_fail(RFX_EUNSUPPORTED, "merge k=%d unsupported", k);
   IVF_HIP(hipGetLastError());
   return RFX_OK;
