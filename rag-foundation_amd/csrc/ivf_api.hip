@@ -432,7 +432,8 @@ int rfx_ivf_search(rfx_ivf_t h, const void* queries_d, int64_t nq, int dtype, in
   rfx::ivf::launch_quantize(queries_d, nq, iv->dim, dtype, qq, qinv, st);
   if (rfx::ivf::launch_coarse_scores(qq, nq, iv->qc, iv->nlist, iv->dim, iv->fc, S, Sid, st))
     return api_fail(RFX_EUNSUPPORTED, "coarse scoring launch rejected");
-  if (rfx::launch_topk_merge(S, Sid, 0, nq, iv->nlist, nprobe, 0, ps, pid, st))
+  if (rfx::ivf::launch_probe_select(S, nq, iv->nlist, nprobe, ps, pid, st) != 0 &&
+      rfx::launch_topk_merge(S, Sid, 0, nq, iv->nlist, nprobe, 0, ps, pid, st))
     return api_fail(RFX_EUNSUPPORTED, "probe selection rejected (nprobe=%d)", nprobe);
   if (rfx::ivf::launch_group_pairs(pid, (int)(nq * nprobe), iv->nlist, poff, pairs, st))
     return api_fail(RFX_EUNSUPPORTED, "pair grouping rejected");

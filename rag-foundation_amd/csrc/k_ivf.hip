@@ -771,6 +771,72 @@ int launch_list_scan(int K, int D, int m, int splits, const int8_t* codes, const
   return -1;
 }
 
+// ---- probe selection: each query's nprobe best coarse scores (round 6) ----------------------------
+// One 256-thread block per query, up to kProbeMaxLists scores held in registers (16 per thread, list
+// c = tid + 256 i).  v = the nprobe-th largest orderable score by a bitwise search on block-wide ballot
+// counts; ties at v are taken by the smallest list ids (a second bitwise search over the tied ids): the
+// set the merge kernel's (score desc, id asc) top-nprobe returns.  The probes are written in no particular
+// order (the pairs are grouped by list next, and every later step is order-free).
+constexpr int kProbeMaxLists = 4096;
+__global__ __launch_bounds__(256) void probe_select_kernel(const float* __restrict__ S, int m, int nprobe,
+                                                           float* __restrict__ ps, int64_t* __restrict__ pid) {
+  constexpr int PT = kProbeMaxLists / 256;
+  __shared__ int wc[2][4];
+  __shared__ int npos;
+  const int tid = threadIdx.x, w = tid >> 6;
+  const int64_t q = blockIdx.x;
+  uint32_t key[PT];
+#pragma unroll
+  for (int i = 0; i < PT; ++i) {
+    const int c = tid + 256 * i;
+    key[i] = c < m ? ord_f32(S[q * m + c]) : 0u;
+  }
+  if (tid == 0) npos = 0;
+  // block-wide count of the keys meeting pred (two LDS slots alternate, so one barrier per count)
+  int par = 0;
+  auto block_count = [&](auto pred) {
+    int cnt = 0;
+#pragma unroll
+    for (int i = 0; i < PT; ++i) cnt += (int)__popcll(__ballot(pred(i)));
+    if ((tid & 63) == 0) wc[par][w] = cnt;
+    __syncthreads();
+    const int t = wc[par][0] + wc[par][1] + wc[par][2] + wc[par][3];
+    par ^= 1;
+    return t;
+  };
+  uint32_t v = 0u;
+  for (int bit = 31; bit >= 0; --bit) {
+    const uint32_t c1 = v | (1u << bit);
+    if (block_count([&](int i) { return key[i] >= c1; }) >= nprobe) v = c1;
+  }
+  const int room = nprobe - block_count([&](int i) { return key[i] > v; });
+  const int ntie = block_count([&](int i) { return key[i] == v; });
+  uint32_t g2 = 0xffffffffu;  // tied ids <= g2 are kept
+  if (ntie > room) {
+    g2 = 0u;
+    for (int bit = 12; bit >= 0; --bit) {  // ids < 4096
+      const uint32_t c1 = g2 | (1u << bit);
+      if (block_count([&](int i) { return key[i] == v && (uint32_t)(tid + 256 * i) < c1; }) < room) g2 = c1;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < PT; ++i) {
+    const int c = tid + 256 * i;
+    const bool keep = c < m && (key[i] > v || (key[i] == v && (uint32_t)c <= g2));
+    if (keep) {
+      const int o = atomicAdd(&npos, 1);
+      ps[q * nprobe + o] = S[q * m + c];
+      pid[q * nprobe + o] = c;
+    }
+  }
+}
+
+int launch_probe_select(const float* S, int64_t nq, int m, int nprobe, float* ps, int64_t* pid, hipStream_t st) {
+  if (m > kProbeMaxLists || nprobe < 1 || nprobe > m || nq <= 0) return -1;
+  hipLaunchKernelGGL(probe_select_kernel, dim3((unsigned)nq), dim3(256), 0, st, S, m, nprobe, ps, pid);
+  return 0;
+}
+
 int launch_group_pairs(const int64_t* probes, int P, int m, int* pair_off, int* pairs, hipStream_t st) {
   if (m > kMaxListsGroup) return -1;
   hipLaunchKernelGGL(group_pairs_kernel, dim3(1), dim3(1024), 0, st, probes, P, m, pair_off, pairs);

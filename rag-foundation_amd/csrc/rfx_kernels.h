@@ -193,6 +193,8 @@ int launch_build_lists(const int* labels, int64_t n, int m, const int8_t* codes,
                        size_t sort_tmp_bytes, int* counts, int64_t* off, int8_t* dcodes, float* dinv,
                        hipStream_t st);
 int list_k(int k);
+// each query's nprobe best of m coarse scores (m <= 4096; else -1: use launch_topk_merge), in no order
+int launch_probe_select(const float* S, int64_t nq, int m, int nprobe, float* ps, int64_t* pid, hipStream_t st);
 int launch_group_pairs(const int64_t* probes, int P, int m, int* pair_off, int* pairs, hipStream_t st);
 int launch_list_scan(int K, int D, int m, int splits, const int8_t* codes, const float* inv, const int* ids, const int64_t* off,
                      const int* pair_off, const int* pairs, int nprobe, const int8_t* qq, const float* qinv,
